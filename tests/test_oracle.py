@@ -1,0 +1,117 @@
+"""Pin the CPU oracle against the golden fixtures produced by the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import ast
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from confild_amd import synth
+from oracle import diffusion as od
+from oracle import siren as osn
+from oracle import unet as ou
+
+SCHED = golden("schedules.npz")
+RESP = {"id": "", "s256": "256", "ddim50": "ddim50", "ddim5": "ddim5", "s8": "8",
+        "s10_20_30": "10,20,30", "s250": "250", "s100": "100"}
+ATTRS = ("betas", "alphas_cumprod", "alphas_cumprod_prev", "sqrt_recip_alphas_cumprod",
+         "sqrt_recipm1_alphas_cumprod", "posterior_variance", "posterior_log_variance_clipped",
+         "posterior_mean_coef1", "posterior_mean_coef2")
+
+
+@pytest.mark.parametrize("sched", ["cosine", "linear"])
+def test_beta_schedule_bitexact(sched):
+    assert np.array_equal(od.beta_schedule(sched, 1000), SCHED[f"{sched}_1000_betas"])
+
+
+@pytest.mark.parametrize("tag", list(RESP))
+def test_respaced_tables_bitexact(tag):
+    tb = od.Tables(1000, "cosine", RESP[tag])
+    assert np.array_equal(tb.timestep_map, SCHED[f"{tag}_timestep_map"])
+    for a in ATTRS:
+        assert np.array_equal(getattr(tb, a), SCHED[f"{tag}_{a}"]), a
+
+
+def test_space_timesteps_errors_and_sections():
+    errs = list(SCHED["space_errors"])
+    for args, want in zip(((1000, "ddim256"), (10, "20"), (100, "ddim7")), errs):
+        try:
+            od.space_timesteps(*args)
+            got = "ok"
+        except ValueError as e:
+            got = "ValueError:" + str(e)
+        assert got == want
+    assert sorted(od.space_timesteps(300, [10, 15, 20])) == list(SCHED["space_300_10_15_20"])
+
+
+def _unet_case(name):
+    g = golden(f"unet_{name}.npz")
+    kw = ast.literal_eval(str(g["kwargs"]))
+    cfg = ou.Config(**kw)
+    shapes = ou.param_shapes(cfg)
+    assert list(shapes) == list(g["keys"])  # same keys, same registration order
+    sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(int(g["seed"]), shapes).items()}
+    return g, cfg, sd
+
+
+@pytest.mark.parametrize("name", ["tiny16", "small32", "heads16", "cfgA32", "cfgB64"])
+def test_unet_forward_matches_reference(name):
+    g, cfg, sd = _unet_case(name)
+    with torch.no_grad():
+        eps = ou.forward(sd, cfg, torch.from_numpy(g["x"]), torch.from_numpy(g["t"])).numpy()
+    ref = g["eps"]
+    err = np.abs(eps - ref).max() / np.abs(ref).max()
+    assert err < 1e-5, err
+
+
+def _tiny_model():
+    g, cfg, sd = _unet_case("tiny16")
+    return lambda x, t: ou.forward(sd, cfg, x, t)
+
+
+@pytest.mark.parametrize("tag,resp,kind", [("ddpm8", "8", "ddpm"), ("ddim5", "ddim5", "ddim")])
+def test_sampler_trajectory_matches_reference(tag, resp, kind):
+    tr = golden(f"traj_{tag}.npz")
+    tb = od.Tables(1000, "cosine", resp)
+    assert np.array_equal(tb.timestep_map, tr["timestep_map"])
+    x, traj = od.sample_loop(tb, _tiny_model(), torch.from_numpy(tr["noise0"]),
+                             torch.from_numpy(tr["noise"]), kind)
+    for k, (xk, xs) in enumerate(traj):
+        assert np.abs(xk.numpy() - tr["samples"][k]).max() < 1e-5, k
+        assert np.abs(xs.numpy() - tr["pred_xstart"][k]).max() < 1e-5, k
+
+
+def test_single_ddpm_step_bitexact():
+    """Given the reference's own eps, one oracle step reproduces the reference sample bit for bit."""
+    tr = golden("traj_ddpm8.npz")
+    tb = od.Tables(1000, "cosine", "8")
+    model = _tiny_model()
+    x = torch.from_numpy(tr["noise0"])
+    t = torch.full((2,), tb.num_timesteps - 1, dtype=torch.int64)
+    with torch.no_grad():
+        eps = model(x, torch.from_numpy(tb.timestep_map)[t])
+    x1, _ = od.ddpm_step(tb, x, t, eps, torch.from_numpy(tr["noise"][0]))
+    assert np.abs(x1.numpy() - tr["samples"][0]).max() < 1e-6
+
+
+@pytest.mark.parametrize("case", ["s2d", "s3d", "caseA", "case4w"])
+def test_siren_matches_reference(case):
+    g = golden(f"siren_{case}.npz")
+    d, L, c, nh, H = (int(v) for v in g["dims"])
+    sd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(int(g["seed"]), d, L, c, nh, H).items()}
+    out = osn.decode(sd, torch.from_numpy(g["coords"]), torch.from_numpy(g["latents"]),
+                     torch.from_numpy(g["xmax"]), torch.from_numpy(g["xmin"]),
+                     torch.from_numpy(g["ymax"]), torch.from_numpy(g["ymin"]))
+    assert np.abs(out.numpy() - g["out"]).max() < 1e-5
+
+
+def test_synth_generator_is_stable():
+    # golden values of the counter-based generator (guards the weight recipe)
+    u = synth.uniform(1234, "input_blocks.0.0.weight", (4,), -1.0, 1.0)
+    assert u.dtype == np.float32
+    v = synth.uniform(1234, "input_blocks.0.0.weight", (4,), -1.0, 1.0)
+    assert np.array_equal(u, v)
+    assert not np.array_equal(u, synth.uniform(1235, "input_blocks.0.0.weight", (4,), -1.0, 1.0))
+    n = synth.normal(7, "x", (10001,))
+    assert abs(float(n.mean())) < 0.05 and abs(float(n.std()) - 1) < 0.05
