@@ -1,0 +1,194 @@
+// Diffusion sampler epilogue (K6), Philox normals and latent de-normalisation.
+//
+// cfd_sched_step replaces, for ModelMeanType.EPSILON + ModelVarType.FIXED_LARGE,
+//   _predict_xstart_from_eps -> clamp(-1,1) -> q_posterior_mean_variance
+//   -> sample = mean + nonzero_mask * exp(0.5*logvar) * noise
+// (U/src/gaussian_diffusion.py:300-314,328-333,208-230,395-439) and the DDIM
+// update (:537-585).  Coefficients are the reference's float64 tables cast to
+// fp32 per timestep (cast done once on the host, _extract_into_tensor :899-912);
+// the elementwise maths is evaluated in the reference's operation order with
+// fp contraction disabled, so for identical (x, eps, noise) the result is the
+// reference's bit for bit.
+#include <string>
+
+#include "common.hpp"
+
+namespace cfd {
+
+struct Philox {
+    static __device__ __forceinline__ uint4 round(uint4 c, uint2 k) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        return make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k.y,
+                          (uint32_t)p0);
+    }
+    static __device__ __forceinline__ uint4 gen(uint64_t seed, uint64_t ctr_lo, uint64_t ctr_hi) {
+        uint4 c = make_uint4((uint32_t)ctr_lo, (uint32_t)(ctr_lo >> 32), (uint32_t)ctr_hi, (uint32_t)(ctr_hi >> 32));
+        uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            c = round(c, k);
+            k.x += 0x9E3779B9u;
+            k.y += 0xBB67AE85u;
+        }
+        return c;
+    }
+    // Four N(0,1) floats for group `grp` of stream (seed, counter).
+    static __device__ __forceinline__ void normal4(uint64_t seed, uint64_t counter, uint64_t grp, float z[4]) {
+        const uint4 r = gen(seed, grp, counter);
+        const float u1 = ((float)r.x + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
+        const float u2 = (float)r.y * 2.3283064365386963e-10f;
+        const float u3 = ((float)r.z + 1.0f) * 2.3283064365386963e-10f;
+        const float u4 = (float)r.w * 2.3283064365386963e-10f;
+        const float r1 = sqrtf(-2.0f * logf(fminf(u1, 1.0f)));
+        const float r2 = sqrtf(-2.0f * logf(fminf(u3, 1.0f)));
+        float s1, c1, s2, c2;
+        sincospif(2.0f * u2, &s1, &c1);
+        sincospif(2.0f * u4, &s2, &c2);
+        z[0] = r1 * c1;
+        z[1] = r1 * s1;
+        z[2] = r2 * c2;
+        z[3] = r2 * s2;
+    }
+};
+
+__global__ void randn_kernel(float* __restrict__ out, int64_t n, uint64_t seed, uint64_t counter) {
+    const int64_t grp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t base = grp * 4;
+    if (base >= n) return;
+    float z[4];
+    Philox::normal4(seed, counter, (uint64_t)grp, z);
+    if (base + 3 < n) {
+        *(f4*)(out + base) = f4{z[0], z[1], z[2], z[3]};  // out 16-B aligned when n % 4 == 0 (checked by caller)
+    } else {
+        for (int j = 0; j < 4 && base + j < n; ++j) out[base + j] = z[j];
+    }
+}
+
+struct StepArgs {
+    const float* coefs;  // (n_t, CFD_NCOEF)
+    const float* x;
+    const float* eps;
+    const int64_t* t;
+    const float* noise;  // may be null -> Philox
+    float* x_out;
+    float* xs_out;       // may be null
+    int64_t n;           // elements per sample
+    int64_t total;       // B * n
+    uint64_t seed, counter;
+    int kind, clip;
+};
+
+__global__ void step_kernel(StepArgs a) {
+#pragma clang fp contract(off)
+    const int64_t grp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t base = grp * 4;
+    if (base >= a.total) return;
+    float z[4];
+    if (a.noise) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z[j] = (base + j < a.total) ? a.noise[base + j] : 0.f;
+    } else {
+        Philox::normal4(a.seed, a.counter, (uint64_t)grp, z);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t i = base + j;
+        if (i >= a.total) break;
+        const int64_t b = i / a.n;
+        const int64_t t = a.t[b];
+        const float* c = a.coefs + t * CFD_NCOEF;
+        const float x = a.x[i], e = a.eps[i];
+        // pred_xstart = sqrt_recip_ac * x - sqrt_recipm1_ac * eps   (:328-333)
+        float xs = c[CFD_COEF_SRA] * x - c[CFD_COEF_SRM1] * e;
+        if (a.clip) xs = fminf(fmaxf(xs, -1.0f), 1.0f);
+        const float mask = t != 0 ? 1.0f : 0.0f;
+        float out;
+        if (a.kind == CFD_STEP_DDPM) {
+            // mean = coef1 * x0 + coef2 * x_t   (:217-220); sample (:431-438)
+            const float mean = c[CFD_COEF_M1] * xs + c[CFD_COEF_M2] * x;
+            out = mean + mask * c[CFD_COEF_SIGMA] * z[j];
+        } else {
+            // eps' = (sra * x - x0) / srm1 (:345-349); mean_pred (:566-570)
+            const float e2 = (c[CFD_COEF_SRA] * x - xs) / c[CFD_COEF_SRM1];
+            const float mean = xs * c[CFD_COEF_SQRT_ABP] + c[CFD_COEF_DIR] * e2;
+            out = mean + mask * c[CFD_COEF_SIGMA_DDIM] * z[j];
+        }
+        a.x_out[i] = out;
+        if (a.xs_out) a.xs_out[i] = xs;
+    }
+}
+
+__global__ void latent_denorm_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                     const float* __restrict__ vmax, const float* __restrict__ vmin, int64_t period) {
+#pragma clang fp contract(off)
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t k = i % period;
+    // (gen + 1) * (max - min) / 2. + min   (scripts/inference.py:61)
+    y[i] = (x[i] + 1.0f) * (vmax[k] - vmin[k]) / 2.0f + vmin[k];
+}
+
+}  // namespace cfd
+
+struct cfd_sched {
+    float* coefs = nullptr;
+    int n_t = 0;
+    int device = 0;
+};
+
+extern "C" int cfd_sched_create(const float* host_coefs, int n_t, int device, cfd_sched** out) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(host_coefs && out && n_t > 0, CFD_EARG, "bad argument");
+        CFD_HIP(hipSetDevice(device));
+        auto* s = new cfd_sched();
+        s->n_t = n_t;
+        s->device = device;
+        CFD_HIP(hipMalloc(&s->coefs, sizeof(float) * n_t * CFD_NCOEF));
+        CFD_HIP(hipMemcpy(s->coefs, host_coefs, sizeof(float) * n_t * CFD_NCOEF, hipMemcpyHostToDevice));
+        *out = s;
+    });
+}
+
+extern "C" void cfd_sched_destroy(cfd_sched* s) {
+    if (!s) return;
+    (void)hipFree(s->coefs);
+    delete s;
+}
+
+extern "C" int cfd_sched_step(const cfd_sched* s, int kind, int clip, const float* x, const float* eps,
+                              const int64_t* t, const float* noise, uint64_t seed, uint64_t counter, float* x_out,
+                              float* xstart_out, int64_t n_per_sample, int B, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(s && x && eps && t && x_out, CFD_EARG, "null argument");
+        CFD_REQUIRE(kind == CFD_STEP_DDPM || kind == CFD_STEP_DDIM, CFD_EARG, "unknown step kind");
+        CFD_REQUIRE(n_per_sample > 0 && B > 0, CFD_EARG, "empty step");
+        cfd::StepArgs a{s->coefs, x, eps, t, noise, x_out, xstart_out, n_per_sample, n_per_sample * B,
+                        seed, counter, kind, clip};
+        const int64_t groups = cfd::ceil_div(a.total, 4);
+        hipLaunchKernelGGL(cfd::step_kernel, dim3((unsigned)cfd::ceil_div(groups, 256)), dim3(256), 0,
+                           (hipStream_t)stream, a);
+        cfd::check_launch("step_kernel");
+    });
+}
+
+extern "C" int cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(out && n > 0, CFD_EARG, "bad argument");
+        CFD_REQUIRE(((uintptr_t)out & 15) == 0, CFD_EARG, "randn output must be 16-byte aligned");
+        const int64_t groups = cfd::ceil_div(n, 4);
+        hipLaunchKernelGGL(cfd::randn_kernel, dim3((unsigned)cfd::ceil_div(groups, 256)), dim3(256), 0,
+                           (hipStream_t)stream, out, n, seed, counter);
+        cfd::check_launch("randn_kernel");
+    });
+}
+
+extern "C" int cfd_latent_denorm(const float* x, float* y, int64_t n, const float* vmax, const float* vmin,
+                                 int64_t period, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(x && y && vmax && vmin && n > 0 && period > 0, CFD_EARG, "bad argument");
+        hipLaunchKernelGGL(cfd::latent_denorm_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0,
+                           (hipStream_t)stream, x, y, n, vmax, vmin, period);
+        cfd::check_launch("latent_denorm_kernel");
+    });
+}

@@ -1,0 +1,274 @@
+"""Diffusion schedules and the GPU reverse loop (drop-in for U/src/gaussian_diffusion.py).
+
+Host side: the float64 coefficient tables exactly as the reference builds them
+(:18-62, :118-169), cast per timestep to fp32 with the same torch ops as
+``_extract_into_tensor`` (:899-912) and uploaded once.  Device side: each
+reverse step is one U-Net forward (cfd_unet_forward) plus one fused epilogue
+launch (cfd_sched_step: x0 prediction, clamp, posterior mean, noise).
+
+RNG: by default the per-step normals come from the in-kernel Philox stream keyed
+by a seed drawn from torch's default CPU generator at loop start (so
+``torch.manual_seed`` makes runs reproducible).  For parity with a reference run,
+pass ``noise=`` (x_T) and ``step_noise=`` (one tensor per step, in the
+reference's draw order: gaussian_diffusion.py:430/576).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def get_named_beta_schedule(schedule_name, num_diffusion_timesteps):
+    """gaussian_diffusion.py:18-40."""
+    if schedule_name == "linear":
+        scale = 1000 / num_diffusion_timesteps
+        return np.linspace(scale * 0.0001, scale * 0.02, num_diffusion_timesteps, dtype=np.float64)
+    if schedule_name == "cosine":
+        return betas_for_alpha_bar(num_diffusion_timesteps,
+                                   lambda t: math.cos((t + 0.008) / 1.008 * math.pi / 2) ** 2)
+    raise NotImplementedError(f"unknown beta schedule: {schedule_name}")
+
+
+def betas_for_alpha_bar(num_diffusion_timesteps, alpha_bar, max_beta=0.999):
+    """gaussian_diffusion.py:43-62."""
+    out = []
+    for i in range(num_diffusion_timesteps):
+        t1, t2 = i / num_diffusion_timesteps, (i + 1) / num_diffusion_timesteps
+        out.append(min(1 - alpha_bar(t2) / alpha_bar(t1), max_beta))
+    return np.array(out)
+
+
+class ModelMeanType(enum.Enum):
+    PREVIOUS_X = enum.auto()
+    START_X = enum.auto()
+    EPSILON = enum.auto()
+
+
+class ModelVarType(enum.Enum):
+    LEARNED = enum.auto()
+    FIXED_SMALL = enum.auto()
+    FIXED_LARGE = enum.auto()
+    LEARNED_RANGE = enum.auto()
+
+
+class LossType(enum.Enum):
+    MSE = enum.auto()
+    RESCALED_MSE = enum.auto()
+    KL = enum.auto()
+    RESCALED_KL = enum.auto()
+
+    def is_vb(self):
+        return self in (LossType.KL, LossType.RESCALED_KL)
+
+
+# row layout of the fp32 coefficient table (include/confild.h CFD_COEF_*)
+SRA, SRM1, M1, M2, SIGMA, SQRT_ABP, DIR, SIGMA_DDIM = range(8)
+STEP_DDPM, STEP_DDIM = 0, 1
+
+
+class _Sched:
+    """Device copy of one fp32 coefficient table (owns a cfd_sched handle)."""
+
+    def __init__(self, coefs: torch.Tensor, device: int):
+        lib = _lib.lib()
+        self.handle = C.c_void_p()
+        host = coefs.contiguous()
+        _lib.check(lib.cfd_sched_create(C.c_void_p(host.data_ptr()), host.shape[0], device, C.byref(self.handle)),
+                   "cfd_sched_create")
+
+    def __del__(self):
+        try:
+            _lib.load().cfd_sched_destroy(self.handle)
+        except Exception:
+            pass
+
+
+class GaussianDiffusion:
+    """Same constructor and sampling API as the reference GaussianDiffusion (:88-169)."""
+
+    def __init__(self, *, betas, model_mean_type, model_var_type, loss_type, rescale_timesteps=False):
+        self.model_mean_type = model_mean_type
+        self.model_var_type = model_var_type
+        self.loss_type = loss_type
+        self.rescale_timesteps = rescale_timesteps
+        betas = np.array(betas, dtype=np.float64)
+        self.betas = betas
+        assert len(betas.shape) == 1, "betas must be 1-D"
+        assert (betas > 0).all() and (betas <= 1).all()
+        self.num_timesteps = int(betas.shape[0])
+        alphas = 1.0 - betas
+        self.alphas_cumprod = np.cumprod(alphas, axis=0)
+        self.alphas_cumprod_prev = np.append(1.0, self.alphas_cumprod[:-1])
+        self.alphas_cumprod_next = np.append(self.alphas_cumprod[1:], 0.0)
+        self.sqrt_alphas_cumprod = np.sqrt(self.alphas_cumprod)
+        self.sqrt_one_minus_alphas_cumprod = np.sqrt(1.0 - self.alphas_cumprod)
+        self.log_one_minus_alphas_cumprod = np.log(1.0 - self.alphas_cumprod)
+        self.sqrt_recip_alphas_cumprod = np.sqrt(1.0 / self.alphas_cumprod)
+        self.sqrt_recipm1_alphas_cumprod = np.sqrt(1.0 / self.alphas_cumprod - 1)
+        self.posterior_variance = betas * (1.0 - self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_log_variance_clipped = np.log(
+            np.append(self.posterior_variance[1], self.posterior_variance[1:]))
+        self.posterior_mean_coef1 = betas * np.sqrt(self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_mean_coef2 = (1.0 - self.alphas_cumprod_prev) * np.sqrt(alphas) / (1.0 - self.alphas_cumprod)
+        self._scheds = {}
+
+    # -- model wrapping (identity here; SpacedDiffusion remaps) -------------------
+    def _map_timesteps(self, t):
+        if self.rescale_timesteps:
+            raise NotImplementedError("rescale_timesteps=True")
+        return t
+
+    # -- coefficient table ----------------------------------------------------
+    def _logvar_table(self):
+        if self.model_var_type == ModelVarType.FIXED_LARGE:
+            return np.log(np.append(self.posterior_variance[1], self.betas[1:]))   # :278-284
+        if self.model_var_type == ModelVarType.FIXED_SMALL:
+            return self.posterior_log_variance_clipped
+        raise NotImplementedError(f"model_var_type {self.model_var_type} (learned variance) on the HIP path")
+
+    def coef_table(self, eta: float = 0.0) -> torch.Tensor:
+        """(num_timesteps, 8) fp32: the per-timestep scalars the reference extracts with
+        ``th.from_numpy(arr)[t].float()`` and combines with fp32 torch ops."""
+        f = lambda a: torch.from_numpy(np.asarray(a, dtype=np.float64)).float()  # noqa: E731
+        n = self.num_timesteps
+        tab = torch.zeros(n, 8, dtype=torch.float32)
+        tab[:, SRA] = f(self.sqrt_recip_alphas_cumprod)
+        tab[:, SRM1] = f(self.sqrt_recipm1_alphas_cumprod)
+        tab[:, M1] = f(self.posterior_mean_coef1)
+        tab[:, M2] = f(self.posterior_mean_coef2)
+        tab[:, SIGMA] = torch.exp(0.5 * f(self._logvar_table()))                      # :431-438
+        ab, abp = f(self.alphas_cumprod), f(self.alphas_cumprod_prev)
+        sigma = eta * torch.sqrt((1 - abp) / (1 - ab)) * torch.sqrt(1 - ab / abp)     # :559-563
+        tab[:, SQRT_ABP] = torch.sqrt(abp)
+        tab[:, DIR] = torch.sqrt(1 - abp - sigma ** 2)
+        tab[:, SIGMA_DDIM] = sigma
+        return tab
+
+    def _sched(self, device: torch.device, eta: float):
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        key = (dev, float(eta))
+        s = self._scheds.get(key)
+        if s is None:
+            s = _Sched(self.coef_table(eta), dev)
+            self._scheds[key] = s
+        return s
+
+    # -- single steps (public API of the reference) ----------------------------
+    def _check_mean_type(self):
+        if self.model_mean_type != ModelMeanType.EPSILON:
+            raise NotImplementedError(f"model_mean_type {self.model_mean_type} on the HIP path (CoNFiLD uses EPSILON)")
+
+    def _step(self, kind, model, x, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, noise, seed, counter, eta):
+        self._check_mean_type()
+        if denoised_fn is not None or cond_fn is not None:
+            raise NotImplementedError("denoised_fn / cond_fn (use the DPS sampler for conditioning)")
+        if x.device.type != "cuda":
+            raise _lib.CfdError("the HIP sampler needs GPU tensors (no CPU fallback)")
+        model_kwargs = model_kwargs or {}
+        x = x.contiguous()
+        eps = model(x, self._map_timesteps(t), **model_kwargs)
+        if eps.shape != x.shape:
+            raise NotImplementedError("learned-variance model outputs (2C channels) on the HIP path")
+        eps = eps.to(torch.float32).contiguous()
+        out = torch.empty_like(x)
+        xs = torch.empty_like(x)
+        nz = None
+        if noise is not None:
+            nz = noise.to(device=x.device, dtype=torch.float32).contiguous()
+        sched = self._sched(x.device, eta)
+        n = x[0].numel()
+        _lib.check(_lib.load().cfd_sched_step(sched.handle, kind, 1 if clip_denoised else 0, _lib.ptr(x),
+                                              _lib.ptr(eps), _lib.ptr(t), _lib.ptr(nz), seed, counter,
+                                              _lib.ptr(out), _lib.ptr(xs), n, x.shape[0],
+                                              _lib.stream_of(x.device)), "cfd_sched_step")
+        return {"sample": out, "pred_xstart": xs}
+
+    def p_sample(self, model, x, t, clip_denoised=True, denoised_fn=None, cond_fn=None, model_kwargs=None,
+                 noise=None, seed=0, counter=0):
+        """gaussian_diffusion.py:395-439 (noise: explicit normals, else Philox(seed, counter))."""
+        t = t.to(device=x.device, dtype=torch.int64).contiguous()
+        with torch.no_grad():
+            return self._step(STEP_DDPM, model, x, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, noise,
+                              seed, counter, 0.0)
+
+    def ddim_sample(self, model, x, t, clip_denoised=True, denoised_fn=None, cond_fn=None, model_kwargs=None,
+                    eta=0.0, noise=None, seed=0, counter=0):
+        """gaussian_diffusion.py:537-585."""
+        t = t.to(device=x.device, dtype=torch.int64).contiguous()
+        with torch.no_grad():
+            return self._step(STEP_DDIM, model, x, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, noise,
+                              seed, counter, eta)
+
+    # -- loops ------------------------------------------------------------------
+    def _loop(self, kind, model, shape, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs, device,
+              progress, eta, step_noise, seed):
+        if device is None:
+            try:
+                device = next(model.parameters()).device
+            except (AttributeError, StopIteration):
+                device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise _lib.CfdError("the HIP sampler runs on the GPU only; move the model to a HIP device")
+        assert isinstance(shape, (tuple, list))
+        lib = _lib.lib()
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        if noise is not None:
+            img = noise.to(device=device, dtype=torch.float32).contiguous()
+        else:
+            img = torch.empty(*shape, dtype=torch.float32, device=device)
+            _lib.check(lib.cfd_randn(_lib.ptr(img), img.numel(), seed, 1 << 40, _lib.stream_of(device)),
+                       "cfd_randn")
+        indices = list(range(self.num_timesteps))[::-1]
+        if progress:
+            from tqdm.auto import tqdm
+            indices = tqdm(indices)
+        B = shape[0]
+        ts = torch.arange(self.num_timesteps, dtype=torch.int64, device=device)
+        for k, i in enumerate(indices):
+            t = ts[i:i + 1].expand(B).contiguous()
+            nz = None if step_noise is None else step_noise[k]
+            with torch.no_grad():
+                out = self._step(kind, model, img, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, nz,
+                                 seed, k, eta)
+            yield out
+            img = out["sample"]
+
+    def p_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
+                      model_kwargs=None, device=None, progress=False, step_noise=None, seed=None):
+        """gaussian_diffusion.py:441-485."""
+        final = None
+        for s in self.p_sample_loop_progressive(model, shape, noise, clip_denoised, denoised_fn, cond_fn,
+                                                model_kwargs, device, progress, step_noise, seed):
+            final = s
+        return final["sample"]
+
+    def p_sample_loop_progressive(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None,
+                                  cond_fn=None, model_kwargs=None, device=None, progress=False, step_noise=None,
+                                  seed=None):
+        """gaussian_diffusion.py:487-535."""
+        yield from self._loop(STEP_DDPM, model, shape, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
+                              device, progress, 0.0, step_noise, seed)
+
+    def ddim_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
+                         model_kwargs=None, device=None, progress=False, eta=0.0, step_noise=None, seed=None):
+        """gaussian_diffusion.py:625-662."""
+        final = None
+        for s in self.ddim_sample_loop_progressive(model, shape, noise, clip_denoised, denoised_fn, cond_fn,
+                                                   model_kwargs, device, progress, eta, step_noise, seed):
+            final = s
+        return final["sample"]
+
+    def ddim_sample_loop_progressive(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None,
+                                     cond_fn=None, model_kwargs=None, device=None, progress=False, eta=0.0,
+                                     step_noise=None, seed=None):
+        """gaussian_diffusion.py:664-707."""
+        yield from self._loop(STEP_DDIM, model, shape, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
+                              device, progress, eta, step_noise, seed)

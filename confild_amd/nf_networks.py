@@ -1,0 +1,181 @@
+"""SIRENAutodecoder_film drop-in (N/cnf/nf_networks.py:443-495) on the fused HIP kernel.
+
+Parameter tree and state_dict keys are the reference's (``net1.{i}.weight``,
+``net1.{i}.bias``, ``net2.{i}.weight``), so ``checkpoint_*.pt["model_state_dict"]``
+loads unchanged.  ``forward(coords, latents)`` keeps the reference signature and
+broadcasting; ``decode(...)`` additionally fuses the coordinate normaliser and the
+output de-normaliser (Normalizer_ts '-11') into the same launch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+DEFAULT_W0 = 30.0  # N/cnf/initialization.py:5
+
+
+class BatchLinear(nn.Linear):
+    """Parameter holder with the reference layout (components.py:55-76).  Its
+    arithmetic runs inside the fused SIREN kernel, never here."""
+
+    def forward(self, input, params=None):
+        raise _lib.CfdError("BatchLinear is evaluated inside the fused HIP SIREN kernel; call the network instead")
+
+
+def _sine_init(m, w0=DEFAULT_W0):
+    with torch.no_grad():
+        n = m.weight.size(-1)
+        m.weight.uniform_(-math.sqrt(6 / n) / w0, math.sqrt(6 / n) / w0)   # initialization.py:117-125
+
+
+def _first_layer_sine_init(m):
+    with torch.no_grad():
+        n = m.weight.size(-1)
+        m.weight.uniform_(-1 / n, 1 / n)                                     # initialization.py:127-132
+
+
+class SIRENAutodecoder_film(nn.Module):
+    """Constructor as nf_networks.py:447-478 (sine nonlinearity, no premap)."""
+
+    def __init__(self, in_coord_features, in_latent_features, out_features, num_hidden_layers, hidden_features,
+                 outermost_linear=False, nonlinearity="sine", weight_init=None, bias_init=None, premap_mode=None,
+                 **kwargs):
+        super().__init__()
+        if nonlinearity != "sine":
+            raise NotImplementedError(f"nonlinearity {nonlinearity!r}: the fused kernel implements sine only")
+        if premap_mode is not None:
+            raise NotImplementedError("premap_mode (FeatureMapping) is not used by any CoNFiLD recipe")
+        self.in_coord_features = in_coord_features
+        self.in_latent_features = in_latent_features
+        self.out_features = out_features
+        self.num_hidden_layers = num_hidden_layers
+        self.hidden_features = hidden_features
+        self.w0 = DEFAULT_W0
+        self.net1 = nn.ModuleList([BatchLinear(in_coord_features, hidden_features)]
+                                  + [BatchLinear(hidden_features, hidden_features) for _ in range(num_hidden_layers)]
+                                  + [BatchLinear(hidden_features, out_features)])
+        self.net2 = nn.ModuleList([BatchLinear(in_latent_features, hidden_features, bias=False)
+                                   for _ in range(num_hidden_layers + 1)])
+        init = weight_init or _sine_init
+        self.net1.apply(lambda m: init(m) if isinstance(m, BatchLinear) else None)
+        self.net2.apply(lambda m: init(m) if isinstance(m, BatchLinear) else None)
+        _first_layer_sine_init(self.net1[0])
+        _first_layer_sine_init(self.net2[0])
+        if bias_init is not None:
+            self.net2.apply(bias_init)
+        self._handles = {}
+
+    # -- device handle --------------------------------------------------------
+    def _signature(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def _handle(self, device):
+        lib = _lib.lib()
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        entry = self._handles.get(dev)
+        if entry is None:
+            cfg = _lib.SirenCfg(self.in_coord_features, self.in_latent_features, self.out_features,
+                                self.num_hidden_layers, self.hidden_features, self.w0)
+            h = C.c_void_p()
+            _lib.check(lib.cfd_siren_create(C.byref(cfg), dev, C.byref(h)), "cfd_siren_create")
+            entry = [h, None]
+            self._handles[dev] = entry
+        sig = self._signature()
+        if entry[1] != sig:
+            for k, p in self.named_parameters():
+                host = p.detach().to("cpu", torch.float32).contiguous()
+                _lib.check(lib.cfd_siren_set_param(entry[0], k.encode(), C.c_void_p(host.data_ptr()), host.numel()),
+                           f"siren set_param {k}")
+            _lib.check(lib.cfd_siren_ready(entry[0]), "cfd_siren_ready")
+            entry[1] = sig
+        return entry[0]
+
+    # -- forward ----------------------------------------------------------------
+    @staticmethod
+    def _flatten(coords, latents, d, L):
+        if coords.shape[-1] != d:
+            raise ValueError(f"coords last dim {coords.shape[-1]} != in_coord_features {d}")
+        if latents.shape[-1] != L:
+            raise ValueError(f"latents last dim {latents.shape[-1]} != in_latent_features {L}")
+        spatial = tuple(coords.shape[:-1])
+        # reference broadcasting: coords (1, N, d) x latents (b, 1, L) -> (b, N, c);
+        # coords (h, w, d) x latents (b, 1, 1, L) -> (b, h, w, c)
+        if latents.dim() >= 2 and any(s != 1 for s in latents.shape[1:-1]):
+            raise NotImplementedError("latents must be (b, 1, ..., 1, L): one latent per output field")
+        if len(spatial) == latents.dim() - 1 and len(spatial) > 1 and spatial[0] == 1:
+            spatial = spatial[1:]
+        b = latents.shape[0] if latents.dim() >= 2 else 1
+        return coords.reshape(-1, d), latents.reshape(b, L), spatial
+
+    def decode(self, coords, latents, x_normalizer=None, y_normalizer=None):
+        """denorm(NF(norm(coords), latents)) in one fused launch (trainer.infer,
+        N/scripts/train.py:265-279; pass_through_model_batch, inference_function.py:22-48)."""
+        d, L, c = self.in_coord_features, self.in_latent_features, self.out_features
+        dev = latents.device
+        if dev.type != "cuda":
+            raise _lib.CfdError("SIREN decode needs GPU tensors (the HIP path has no CPU fallback)")
+        if latents.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("gradients through the SIREN decoder (DPS) are not built yet")
+        cf, lat, spatial = self._flatten(coords, latents, d, L)
+        cf = cf.to(device=dev, dtype=torch.float32).contiguous()
+        lat = lat.detach().to(torch.float32).contiguous()
+        N = cf.shape[0]
+        xmax = xmin = ymax = ymin = None
+        ystride = 0
+        if x_normalizer is not None:
+            if x_normalizer.method != "-11":
+                cf = x_normalizer.normalize(cf).contiguous()
+            else:
+                xmax = x_normalizer.params[0].to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+                xmin = x_normalizer.params[1].to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+                if xmax.numel() != d:
+                    raise ValueError("coordinate normaliser must have one (max, min) per coordinate feature")
+        post = None
+        if y_normalizer is not None:
+            if y_normalizer.method != "-11":
+                post = y_normalizer
+            else:
+                ymax = y_normalizer.params[0].to(device=dev, dtype=torch.float32)
+                ymin = y_normalizer.params[1].to(device=dev, dtype=torch.float32)
+                if ymax.numel() == c:
+                    ystride = 0
+                elif ymax.numel() == N * c:
+                    ystride = c
+                else:
+                    raise ValueError(f"output normaliser params of {ymax.numel()} values match neither (c) nor (N, c)")
+                ymax = ymax.reshape(-1).contiguous()
+                ymin = ymin.reshape(-1).contiguous()
+        h = self._handle(dev)
+        b = lat.shape[0]
+        nbytes = C.c_size_t()
+        lib = _lib.load()
+        _lib.check(lib.cfd_siren_workspace_bytes(h, b, C.byref(nbytes)), "siren workspace")
+        ws = torch.empty(max(nbytes.value, 16), dtype=torch.uint8, device=dev)
+        out = torch.empty((b, N, c), dtype=torch.float32, device=dev)
+        _lib.check(lib.cfd_siren_forward(h, _lib.ptr(cf), N, _lib.ptr(lat), b, _lib.ptr(xmax), _lib.ptr(xmin),
+                                         _lib.ptr(ymax), _lib.ptr(ymin), ystride, _lib.ptr(out), _lib.ptr(ws),
+                                         ws.numel(), _lib.stream_of(dev)), "cfd_siren_forward")
+        if post is not None:
+            out = post.denormalize(out)
+        return out.reshape((b,) + spatial + (c,))
+
+    def forward(self, coords, latents):
+        """nf_networks.py:480-495 (raw, un-normalised in and out)."""
+        return self.decode(coords, latents)
+
+    def disable_gradient(self):
+        for p in self.parameters():
+            p.requires_grad = False
+
+    def __del__(self):
+        try:
+            lib = _lib.load()
+            for h, _ in self._handles.values():
+                lib.cfd_siren_destroy(h)
+        except Exception:
+            pass

@@ -1,0 +1,290 @@
+"""UNetModel drop-in (U/src/unet.py:396-663) backed by the HIP library.
+
+The module keeps the reference's parameter tree, so ``state_dict()`` /
+``load_state_dict()`` use exactly the reference keys (``time_embed.0.weight``,
+``input_blocks.1.0.in_layers.2.weight``, ...; 368 tensors at 64 px) and an
+``ema_*.pt`` checkpoint of the reference loads unchanged.  ``forward(x, t)``
+runs the whole network as one ``cfd_unet_forward`` call (include/confild.h):
+weights are packed once into kernel layouts on the device and re-packed only
+when a parameter changes.  There is no CPU path: a CPU input raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+def default_channel_mult(image_size: int):
+    """U/src/script_util.py:150-160."""
+    table = {512: (0.5, 1, 1, 2, 2, 4, 4), 256: (1, 1, 2, 2, 4, 4), 128: (1, 1, 2, 3, 4), 64: (1, 2, 3, 4)}
+    if image_size not in table:
+        raise ValueError(f"unsupported image size: {image_size}")
+    return table[image_size]
+
+
+def param_shapes(in_channels, model_channels, out_channels, num_res_blocks, attention_resolutions,
+                 channel_mult, num_heads=1, num_head_channels=-1):
+    """Reference state_dict key -> shape, in registration order (unet.py:469-616)."""
+    mc, tdim = model_channels, model_channels * 4
+    s = {}
+
+    def conv(pre, cin, cout, k=3, one_d=False):
+        s[pre + ".weight"] = (cout, cin, 1) if one_d else (cout, cin, k, k)
+        s[pre + ".bias"] = (cout,)
+
+    def norm(pre, c):
+        s[pre + ".weight"] = (c,)
+        s[pre + ".bias"] = (c,)
+
+    def res(pre, cin, cout):
+        norm(pre + ".in_layers.0", cin)
+        conv(pre + ".in_layers.2", cin, cout)
+        s[pre + ".emb_layers.1.weight"] = (cout, tdim)
+        s[pre + ".emb_layers.1.bias"] = (cout,)
+        norm(pre + ".out_layers.0", cout)
+        conv(pre + ".out_layers.3", cout, cout)
+        if cin != cout:
+            conv(pre + ".skip_connection", cin, cout, 1)
+
+    def attn(pre, c):
+        heads = num_heads if num_head_channels == -1 else c // num_head_channels
+        if heads <= 0 or c % heads:
+            raise ValueError(f"q,k,v channels {c} is not divisible by num_head_channels {num_head_channels}")
+        norm(pre + ".norm", c)
+        conv(pre + ".qkv", c, 3 * c, one_d=True)
+        conv(pre + ".proj_out", c, c, one_d=True)
+
+    s["time_embed.0.weight"] = (tdim, mc)
+    s["time_embed.0.bias"] = (tdim,)
+    s["time_embed.2.weight"] = (tdim, tdim)
+    s["time_embed.2.bias"] = (tdim,)
+    ch = int(channel_mult[0] * mc)
+    conv("input_blocks.0.0", in_channels, ch)
+    chans, ds, idx = [ch], 1, 1
+    for level, mult in enumerate(channel_mult):
+        for _ in range(num_res_blocks):
+            cout = int(mult * mc)
+            res(f"input_blocks.{idx}.0", ch, cout)
+            ch = cout
+            if ds in attention_resolutions:
+                attn(f"input_blocks.{idx}.1", ch)
+            chans.append(ch)
+            idx += 1
+        if level != len(channel_mult) - 1:
+            conv(f"input_blocks.{idx}.0.op", ch, ch)
+            chans.append(ch)
+            ds *= 2
+            idx += 1
+    res("middle_block.0", ch, ch)
+    attn("middle_block.1", ch)
+    res("middle_block.2", ch, ch)
+    idx = 0
+    for level, mult in list(enumerate(channel_mult))[::-1]:
+        for i in range(num_res_blocks + 1):
+            ich = chans.pop()
+            cout = int(mc * mult)
+            res(f"output_blocks.{idx}.0", ch + ich, cout)
+            ch = cout
+            j = 1
+            if ds in attention_resolutions:
+                attn(f"output_blocks.{idx}.1", ch)
+                j = 2
+            if level and i == num_res_blocks:
+                conv(f"output_blocks.{idx}.{j}.conv", ch, ch)
+                ds //= 2
+            idx += 1
+    norm("out.0", ch)
+    conv("out.2", int(channel_mult[0] * mc), out_channels)
+    return s
+
+
+def _zero_init_keys(keys):
+    """Modules the reference wraps in zero_module (unet.py:210-212,294,615)."""
+    out = set()
+    for k in keys:
+        if ".out_layers.3." in k or ".proj_out." in k or k.startswith("out.2."):
+            out.add(k)
+    return out
+
+
+class _Node(nn.Module):
+    """Parameter-only container mirroring one reference submodule path."""
+
+    def forward(self, *a, **k):  # pragma: no cover - never called
+        raise RuntimeError("parameter container")
+
+
+def _build_tree(root: nn.Module, shapes: dict):
+    for key, shape in shapes.items():
+        parts = key.split(".")
+        node = root
+        for p in parts[:-1]:
+            child = node._modules.get(p)
+            if child is None:
+                child = _Node()
+                node.add_module(p, child)
+            node = child
+        node.register_parameter(parts[-1], nn.Parameter(torch.empty(shape)))
+
+
+class UNetModel(nn.Module):
+    """Same constructor as the reference UNetModel (unet.py:427-449).
+
+    Supported: the configuration every CoNFiLD recipe uses (dims=2,
+    conv_resample=True, legacy attention order, no class conditioning, no
+    scale-shift norm, no resblock up/down).  Other options raise
+    NotImplementedError instead of silently computing something else.
+    """
+
+    def __init__(self, image_size, in_channels, model_channels, out_channels, num_res_blocks,
+                 attention_resolutions, dropout=0, channel_mult=(1, 2, 4, 8), conv_resample=True, dims=2,
+                 num_classes=None, use_checkpoint=False, use_fp16=False, num_heads=1, num_head_channels=-1,
+                 num_heads_upsample=-1, use_scale_shift_norm=False, resblock_updown=False,
+                 use_new_attention_order=False):
+        super().__init__()
+        unsupported = {"num_classes": num_classes is not None, "use_scale_shift_norm": use_scale_shift_norm,
+                       "resblock_updown": resblock_updown, "use_new_attention_order": use_new_attention_order,
+                       "conv_resample=False": not conv_resample, "dims!=2": dims != 2,
+                       "num_heads_upsample": num_heads_upsample not in (-1, num_heads),
+                       "non-integer channel_mult": any(float(m) != int(m) for m in channel_mult)}
+        bad = [k for k, v in unsupported.items() if v]
+        if bad:
+            raise NotImplementedError(f"UNetModel options not implemented on the HIP path: {bad}")
+        if use_fp16:
+            raise NotImplementedError("use_fp16: the HIP U-Net computes fp32 (bf16 MFMA variant is a later row)")
+        self.image_size = image_size
+        self.in_channels = in_channels
+        self.model_channels = model_channels
+        self.out_channels = out_channels
+        self.num_res_blocks = num_res_blocks
+        self.attention_resolutions = tuple(attention_resolutions)
+        self.dropout = dropout
+        self.channel_mult = tuple(int(m) for m in channel_mult)
+        self.num_heads = num_heads
+        self.num_head_channels = num_head_channels
+        self.dtype = torch.float32
+        shapes = param_shapes(in_channels, model_channels, out_channels, num_res_blocks,
+                              self.attention_resolutions, self.channel_mult, num_heads, num_head_channels)
+        self._shapes = shapes
+        _build_tree(self, shapes)
+        self._reset_parameters()
+        self._handles = {}      # device index -> (handle ptr, uploaded signature)
+        self._workspaces = {}   # (device, B) -> uint8 tensor
+
+    # -- initialisation (reference: PyTorch defaults + zero_module) ----------
+    @torch.no_grad()
+    def _reset_parameters(self):
+        zero = _zero_init_keys(self._shapes)
+        sd = dict(self.named_parameters())
+        for k, p in sd.items():
+            if k in zero:
+                p.zero_()
+            elif p.dim() == 1 and (k.endswith("in_layers.0.weight") or k.endswith("out_layers.0.weight")
+                                   or k.endswith("norm.weight") or k == "out.0.weight"):
+                p.fill_(1.0)
+            elif p.dim() == 1 and (k.endswith("in_layers.0.bias") or k.endswith("out_layers.0.bias")
+                                   or k.endswith("norm.bias") or k == "out.0.bias"):
+                p.zero_()
+            else:
+                wk = k[:-4] + "weight" if k.endswith("bias") else k
+                fan_in = int(np.prod(self._shapes[wk][1:]))
+                b = 1.0 / math.sqrt(fan_in)
+                p.uniform_(-b, b)
+
+    # -- device handle ----------------------------------------------------------
+    def _cfg_struct(self):
+        cfg = _lib.UNetCfg()
+        cfg.image_size = self.image_size
+        cfg.in_channels = self.in_channels
+        cfg.model_channels = self.model_channels
+        cfg.out_channels = self.out_channels
+        cfg.num_res_blocks = self.num_res_blocks
+        cfg.n_mult = len(self.channel_mult)
+        for i, m in enumerate(self.channel_mult):
+            cfg.channel_mult[i] = m
+        cfg.n_attn = len(self.attention_resolutions)
+        for i, d in enumerate(self.attention_resolutions):
+            cfg.attention_ds[i] = d
+        cfg.num_heads = self.num_heads
+        cfg.num_head_channels = self.num_head_channels
+        return cfg
+
+    def _signature(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def _handle(self, device: torch.device):
+        lib = _lib.lib()
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        entry = self._handles.get(dev)
+        if entry is None:
+            h = C.c_void_p()
+            with torch.cuda.device(dev):
+                _lib.check(lib.cfd_unet_create(C.byref(self._cfg_struct()), dev, C.byref(h)), "cfd_unet_create")
+            entry = [h, None]
+            self._handles[dev] = entry
+            # timestep frequencies computed exactly as nn.py:129-131 (torch, fp32)
+            half = self.model_channels // 2
+            fr = torch.exp(-math.log(10000) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
+            fr = fr.contiguous()
+            _lib.check(lib.cfd_unet_set_time_freqs(h, C.c_void_p(fr.data_ptr()), half), "set_time_freqs")
+        sig = self._signature()
+        if entry[1] != sig:
+            h = entry[0]
+            for k, p in self.named_parameters():
+                host = p.detach().to("cpu", torch.float32).contiguous()
+                _lib.check(lib.cfd_unet_set_param(h, k.encode(), C.c_void_p(host.data_ptr()), host.numel()),
+                           f"set_param {k}")
+            _lib.check(lib.cfd_unet_ready(h), "cfd_unet_ready")
+            entry[1] = sig
+        return entry[0]
+
+    def _workspace(self, h, device, B):
+        key = (device, B)
+        ws = self._workspaces.get(key)
+        if ws is None:
+            n = C.c_size_t()
+            _lib.check(_lib.load().cfd_unet_workspace_bytes(h, B, C.byref(n)), "workspace_bytes")
+            ws = torch.empty(n.value, dtype=torch.uint8, device=device)
+            self._workspaces = {key: ws}  # keep one workspace (largest recent B)
+        return ws
+
+    def forward(self, x: torch.Tensor, timesteps: torch.Tensor, y=None) -> torch.Tensor:
+        """UNetModel.forward (unet.py:634-663): (B, C, H, W) fp32, (B,) timesteps -> eps."""
+        if y is not None:
+            raise NotImplementedError("class-conditional U-Net is not part of the CoNFiLD path")
+        if x.device.type != "cuda":
+            raise _lib.CfdError("UNetModel.forward: input must be on the GPU (the HIP path has no CPU fallback)")
+        if x.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("input gradients through the U-Net (DPS adjoint, SURVEY 8f rank 1) "
+                                      "are not built yet")
+        B, Cin, H, W = x.shape
+        if Cin != self.in_channels or H != self.image_size or W != self.image_size:
+            raise ValueError(f"expected (B, {self.in_channels}, {self.image_size}, {self.image_size}), got "
+                             f"{tuple(x.shape)}")
+        x = x.detach().to(torch.float32).contiguous()
+        if timesteps.is_floating_point():
+            if not torch.equal(timesteps, timesteps.round()):
+                raise NotImplementedError("fractional timesteps (rescale_timesteps=True) are not supported")
+        t = timesteps.to(device=x.device, dtype=torch.int64).contiguous()
+        if t.shape != (B,):
+            raise ValueError("timesteps must have shape (B,)")
+        h = self._handle(x.device)
+        ws = self._workspace(h, x.device, B)
+        eps = torch.empty((B, self.out_channels, H, W), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().cfd_unet_forward(h, _lib.ptr(x), _lib.ptr(t), _lib.ptr(eps), B, _lib.ptr(ws),
+                                                ws.numel(), _lib.stream_of(x.device)), "cfd_unet_forward")
+        return eps
+
+    def __del__(self):
+        try:
+            lib = _lib.load()
+            for h, _ in self._handles.values():
+                lib.cfd_unet_destroy(h)
+        except Exception:
+            pass

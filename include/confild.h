@@ -1,0 +1,147 @@
+/*
+ * confild.h -- C ABI of libconfild_hip.so, the MI355X (gfx950) implementation of
+ * CoNFiLD's generation hot path.
+ *
+ * The reference (semihkacmaz/CoNFiLD, pure Python) has no native FFI: its
+ * boundary is a set of Python callables.  Each entry point below replaces the
+ * arithmetic behind one of them; the Python mirror in confild_amd/ binds these
+ * with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - plain pointers and sizes only; no framework types;
+ *   - tensor pointers are DEVICE pointers on the handle's device unless the
+ *     parameter name says host_; fp32 throughout (the reference computes fp32);
+ *   - activations are NHWC ("channels last"); the U-Net's (B,1,H,W) input and
+ *     output are identical in NCHW and NHWC because C == 1;
+ *   - every call is stream-ordered on `stream` (a hipStream_t, NULL = default)
+ *     and performs no host synchronisation, no allocation and no host<->device
+ *     copy, except the *_create / *_set_param / cfd_sched_create calls;
+ *   - return 0 on success, a CFD_E* code otherwise; cfd_last_error() gives a
+ *     thread-local message.
+ */
+#ifndef CONFILD_H
+#define CONFILD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { CFD_OK = 0, CFD_EARG = 1, CFD_EHIP = 2, CFD_EKEY = 3, CFD_ESHAPE = 4, CFD_ESTATE = 5 };
+
+const char* cfd_last_error(void);
+/* Returns the library build tag ("gfx950 ..."); used to prove which .so is loaded. */
+const char* cfd_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* Latent U-Net (replaces UNetModel, U/src/unet.py:396-663, built by         */
+/* create_model, U/src/script_util.py:130-187).                              */
+/* ------------------------------------------------------------------------ */
+typedef struct cfd_unet cfd_unet;
+
+typedef struct {
+    int image_size;          /* informational; H == W == image_size expected   */
+    int in_channels;         /* 1 in every CoNFiLD recipe                      */
+    int model_channels;      /* num_channels                                   */
+    int out_channels;        /* 1 (learn_sigma=False)                          */
+    int num_res_blocks;
+    int n_mult;              /* len(channel_mult)                              */
+    int channel_mult[8];
+    int n_attn;              /* len(attention downsample rates)                */
+    int attention_ds[8];     /* image_size // res for res in attention_resolutions */
+    int num_heads;
+    int num_head_channels;   /* -1 => use num_heads                            */
+} cfd_unet_cfg;
+
+/* Builds the topology of UNetModel.__init__ (unet.py:427-616) on `device`. */
+int  cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** out);
+void cfd_unet_destroy(cfd_unet* h);
+/* Parameter registry in the reference's state_dict order and key names. */
+int  cfd_unet_num_params(const cfd_unet* h, int* n);
+int  cfd_unet_param_info(const cfd_unet* h, int idx, const char** key, int* ndim, int64_t shape[4]);
+/* Copies one reference-layout fp32 tensor (torch (Cout,Cin,kh,kw) etc.) from
+ * HOST memory and packs it into the kernel layout.  Replaces load_state_dict. */
+int  cfd_unet_set_param(cfd_unet* h, const char* key, const float* host_data, size_t n);
+/* Overrides the (model_channels/2) timestep-embedding frequencies
+ * exp(-ln(1e4) * i / half) (nn.py:129-131) with host-computed fp32 values so
+ * they match the caller's framework bit for bit (default: computed in C++). */
+int  cfd_unet_set_time_freqs(cfd_unet* h, const float* host_freqs, int n);
+/* Fails with CFD_ESTATE until every parameter has been set. */
+int  cfd_unet_ready(const cfd_unet* h);
+int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
+/* eps = UNetModel.forward(x, timesteps): x (B,1,H,W), t (B) int64 (already
+ * remapped through timestep_map, respace.py:123-128), eps (B,1,H,W). */
+int  cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
+                      void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Diffusion step epilogue (replaces p_mean_variance + p_sample / ddim_sample */
+/* for EPSILON / FIXED_LARGE, U/src/gaussian_diffusion.py:232-326,395-439,    */
+/* 537-585).                                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct cfd_sched cfd_sched;
+enum { CFD_COEF_SRA = 0, CFD_COEF_SRM1, CFD_COEF_M1, CFD_COEF_M2, CFD_COEF_SIGMA,
+       CFD_COEF_SQRT_ABP, CFD_COEF_DIR, CFD_COEF_SIGMA_DDIM, CFD_NCOEF };
+enum { CFD_STEP_DDPM = 0, CFD_STEP_DDIM = 1 };
+
+/* host_coefs: n_t rows of CFD_NCOEF fp32 values, the float64 tables of the
+ * (respaced) process already cast to fp32 the way _extract_into_tensor does
+ * (gaussian_diffusion.py:899-912). */
+int  cfd_sched_create(const float* host_coefs, int n_t, int device, cfd_sched** out);
+void cfd_sched_destroy(cfd_sched* s);
+/* x_out = step(x, eps, t).  t: (B) int64 device indices into the table.
+ * noise: (B*n) device normals in the reference's draw order, or NULL to draw
+ * them in-kernel with Philox4x32-10 keyed by (seed, counter).
+ * xstart_out may be NULL.  x_out may alias x. */
+int  cfd_sched_step(const cfd_sched* s, int kind, int clip, const float* x, const float* eps,
+                    const int64_t* t, const float* noise, uint64_t seed, uint64_t counter,
+                    float* x_out, float* xstart_out, int64_t n_per_sample, int B, void* stream);
+/* (B*n) standard normals from Philox4x32-10 (seed, counter): the device-side
+ * stand-in for th.randn (gaussian_diffusion.py:513). */
+int  cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, void* stream);
+/* Latent de-normalisation (scripts/inference.py:59-61): y = (x+1)*(max-min)/2 + min,
+ * max/min broadcast over the trailing `period` elements (period=1: scalars). */
+int  cfd_latent_denorm(const float* x, float* y, int64_t n, const float* vmax, const float* vmin,
+                       int64_t period, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Conditional neural field decoder: SIRENAutodecoder_film                    */
+/* (N/cnf/nf_networks.py:443-495, BatchLinear/Sine components.py:19-25,55-76) */
+/* fused with Normalizer_ts '-11' (N/cnf/utils/normalize.py:100-114).         */
+/* ------------------------------------------------------------------------ */
+typedef struct cfd_siren cfd_siren;
+
+typedef struct {
+    int in_coord_features;   /* d  (<= 4)                                     */
+    int in_latent_features;  /* L                                            */
+    int out_features;        /* c  (<= 4)                                     */
+    int num_hidden_layers;   /* nh                                           */
+    int hidden_features;     /* H  (multiple of 16, <= 512)                  */
+    float w0;                /* 30 (DEFAULT_W0)                              */
+} cfd_siren_cfg;
+
+int  cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren** out);
+void cfd_siren_destroy(cfd_siren* h);
+int  cfd_siren_num_params(const cfd_siren* h, int* n);
+int  cfd_siren_param_info(const cfd_siren* h, int idx, const char** key, int* ndim, int64_t shape[4]);
+/* keys net1.{i}.weight/bias, net2.{i}.weight (host fp32, reference layout). */
+int  cfd_siren_set_param(cfd_siren* h, const char* key, const float* host_data, size_t n);
+int  cfd_siren_ready(const cfd_siren* h);
+int  cfd_siren_workspace_bytes(const cfd_siren* h, int b, size_t* bytes);
+/* out (b, N, c) = denorm( NF( norm(coords), latents ) ).
+ *   coords (N, d); latents (b, L);
+ *   xmax/xmin: (d) coordinate normaliser params, or NULL (coords already normalised);
+ *   ymax/ymin: output normaliser params with row stride y_stride (elements) per
+ *              coordinate: y_stride = c for a per-point (N, c) table (lumped
+ *              latent, train.py:194-201), 0 for a (c) table; NULL = raw output. */
+int  cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, const float* latents, int b,
+                       const float* xmax, const float* xmin,
+                       const float* ymax, const float* ymin, int64_t y_stride,
+                       float* out, void* workspace, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CONFILD_H */

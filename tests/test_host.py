@@ -1,0 +1,151 @@
+"""CPU tests of the host side: library exports, reference key layout, schedule
+tables, factories and failure behaviour.  No GPU calls."""
+import ast
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, golden
+from confild_amd import _lib
+from confild_amd import gaussian_diffusion as gd
+from confild_amd.respace import space_timesteps
+from confild_amd.script_util import create_gaussian_diffusion, create_model
+from oracle import diffusion as od
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    hdr = open(os.path.join(ROOT, "include", "confild.h")).read()
+    declared = set(re.findall(r"\b(cfd_[a-z_0-9]+)\s*\(", hdr))
+    assert declared, "no declarations parsed"
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert declared == set(_lib.EXPORTS)
+    assert b"gfx950" in lib.cfd_version()
+
+
+def test_so_contains_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_no_cpu_fallback():
+    m = create_model(image_size=16, num_channels=32, num_res_blocks=1, channel_mult="1,2", num_heads=4,
+                     num_head_channels=16, attention_resolutions="8")
+    with pytest.raises(_lib.CfdError):
+        m(torch.zeros(1, 1, 16, 16), torch.zeros(1, dtype=torch.int64))
+
+
+@pytest.mark.parametrize("name", ["tiny16", "small32", "heads16", "cfgA32", "cfgB64", "cfgE128"])
+def test_unet_state_dict_keys_match_reference(name):
+    g = golden(f"unet_{name}.npz")
+    kw = ast.literal_eval(str(g["kwargs"]))
+    m = create_model(**kw)
+    sd = m.state_dict()
+    assert list(sd.keys()) == list(g["keys"])
+    assert sum(v.numel() for v in sd.values()) == int(g["nparams"])
+
+
+def test_create_model_errors_like_reference():
+    with pytest.raises(ValueError):
+        create_model(image_size=384, num_channels=128, num_res_blocks=2)  # no default mult (script_util.py:160)
+    with pytest.raises(NotImplementedError):
+        create_model(image_size=64, num_channels=128, num_res_blocks=2, use_scale_shift_norm=True)
+
+
+RESP = {"id": "", "s256": "256", "ddim50": "ddim50", "ddim5": "ddim5", "s8": "8", "s10_20_30": "10,20,30"}
+
+
+@pytest.mark.parametrize("tag", list(RESP))
+def test_product_tables_bitexact_vs_reference(tag):
+    S = golden("schedules.npz")
+    d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=RESP[tag])
+    assert np.array_equal(np.array(d.timestep_map), S[f"{tag}_timestep_map"])
+    for a in ("betas", "alphas_cumprod", "alphas_cumprod_prev", "sqrt_recip_alphas_cumprod",
+              "sqrt_recipm1_alphas_cumprod", "posterior_variance", "posterior_log_variance_clipped",
+              "posterior_mean_coef1", "posterior_mean_coef2"):
+        assert np.array_equal(getattr(d, a), S[f"{tag}_{a}"]), a
+
+
+def test_space_timesteps_matches_reference_errors():
+    S = golden("schedules.npz")
+    for args, want in zip(((1000, "ddim256"), (10, "20"), (100, "ddim7")), list(S["space_errors"])):
+        try:
+            space_timesteps(*args)
+            got = "ok"
+        except ValueError as e:
+            got = "ValueError:" + str(e)
+        assert got == want
+
+
+def test_coef_table_matches_oracle_step_scalars():
+    """The fp32 per-step scalars the kernel uses are exactly the reference's
+    extracted-and-cast values (checked through the oracle's formulas)."""
+    d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="256")
+    tab = d.coef_table()
+    tb = od.Tables(1000, "cosine", "256")
+    f = lambda a: torch.from_numpy(a).float()  # noqa: E731
+    assert torch.equal(tab[:, gd.SRA], f(tb.sqrt_recip_alphas_cumprod))
+    assert torch.equal(tab[:, gd.SRM1], f(tb.sqrt_recipm1_alphas_cumprod))
+    assert torch.equal(tab[:, gd.M1], f(tb.posterior_mean_coef1))
+    assert torch.equal(tab[:, gd.M2], f(tb.posterior_mean_coef2))
+    assert torch.equal(tab[:, gd.SIGMA], torch.exp(0.5 * f(tb.fixed_large_logvar)))
+
+
+def test_step_arithmetic_emulation_bitexact():
+    """Emulate the kernel's fp32 operation order on the CPU (no FMA) and compare
+    with the oracle step bit for bit: documents why the GPU step is bit-exact."""
+    tr = golden("traj_ddpm8.npz")
+    d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="8")
+    tab = d.coef_table().numpy()
+    tb = od.Tables(1000, "cosine", "8")
+    x = tr["noise0"]
+    eps = np.random.default_rng(0).standard_normal(x.shape).astype(np.float32)
+    z = tr["noise"][0]
+    t = 7
+    c = tab[t]
+    xs = np.clip(c[gd.SRA] * x - c[gd.SRM1] * eps, -1, 1).astype(np.float32)
+    mean = c[gd.M1] * xs + c[gd.M2] * x
+    out = mean + np.float32(1.0) * c[gd.SIGMA] * z
+    ref, _ = od.ddpm_step(tb, torch.from_numpy(x), torch.full((2,), t), torch.from_numpy(eps), torch.from_numpy(z))
+    assert np.array_equal(out, ref.numpy())
+
+
+def test_siren_state_dict_keys_match_reference_layout():
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    net = SIRENAutodecoder_film(3, 384, 3, 15, 384)
+    keys = list(net.state_dict().keys())
+    assert keys[0] == "net1.0.weight" and keys[-1] == "net2.15.weight"
+    assert net.state_dict()["net1.16.weight"].shape == (3, 384)
+    assert sum(v.numel() for v in net.state_dict().values()) == 4579587  # reference SIRENAutodecoder_film(3,384,3,15,384)
+
+
+def test_trainer_loads_reference_files(tmp_path):
+    import yaml
+    from confild_amd import synth
+    from confild_amd.read_input import basic_input
+    from confild_amd.trainer import trainer
+    sd = synth.siren_state_dict(5, 3, 8, 3, 2, 32)
+    torch.save({"x_normalizer_params": (torch.ones(1, 3), torch.zeros(1, 3)),
+                "y_normalizer_params": (torch.ones(1, 5, 3), -torch.ones(1, 5, 3))},
+               tmp_path / "normalizer_params.pt")
+    for ep in (2, 11):
+        torch.save({"epoch": ep, "model_state_dict": {k: torch.from_numpy(v) for k, v in sd.items()},
+                    "optim_net_dec_dict": {}, "optim_states_dict": {}, "hidden_states": {}},
+                   tmp_path / f"checkpoint_{ep}.pt")
+    cfg = {"save_path": str(tmp_path), "lumped_latent": True, "normalizer": {"method": "-11", "dim": 0},
+           "multiGPU": 1, "hidden_size": 8, "dims": 3,
+           "NF": {"name": "SIRENAutodecoder_film", "out_features": 3, "num_hidden_layers": 2, "hidden_features": 32}}
+    (tmp_path / "c.yml").write_text(yaml.safe_dump(cfg))
+    tr = trainer(basic_input(str(tmp_path / "c.yml")), infer_mode=True)
+    tr.load(-1, siren_only=True)
+    assert tr.start_epoch == 11
+    assert torch.equal(tr.nf.state_dict()["net1.1.weight"], torch.from_numpy(sd["net1.1.weight"]))
+    with pytest.raises(FileNotFoundError):
+        cfg["save_path"] = str(tmp_path / "missing")
+        (tmp_path / "d.yml").write_text(yaml.safe_dump(cfg))
+        trainer(basic_input(str(tmp_path / "d.yml")), infer_mode=True)
