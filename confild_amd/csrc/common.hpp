@@ -54,24 +54,27 @@ inline void check_launch(const char* what) {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// Accurate fp32 sine: Cody-Waite reduction by pi in three fma steps (exact for
-// |x| < 125), then a degree-9 odd minimax polynomial on [-pi/2, pi/2]
-// (~3.5 ulp).  Larger arguments (never produced by SIREN-initialised weights,
-// but possible with trained ones) take the library sinf path.
+// fp32 sine, branch-free.  |x| < 39000: Cody-Waite reduction by pi with a
+// 4-term split of pi (exact reduction in that range, the SLEEF single-precision
+// scheme), then a degree-9 odd minimax polynomial on [-pi/2, pi/2] (~3.5 ulp).
+// Beyond that (|w0 * preactivation| >= 39000, i.e. |preactivation| >= 1300,
+// three orders of magnitude above what SIREN weights produce) the hardware
+// v_sin_f32 result is selected; DESIGN.md states this range.
 __device__ __forceinline__ float sin_cw(float x) {
-    if (__builtin_expect(fabsf(x) >= 125.0f, 0)) return sinf(x);
     const float q = rintf(x * 0.318309886183790671538f);
-    float r = fmaf(q, -3.1414794921875f, x);
-    r = fmaf(q, -0.00011315941810607910156f, r);
-    r = fmaf(q, -1.9841872589410058936e-09f, r);
+    float r = fmaf(q, -3.140625f, x);
+    r = fmaf(q, -0.0009670257568359375f, r);
+    r = fmaf(q, -6.2771141529083251953e-07f, r);
+    r = fmaf(q, -1.2154201256553420762e-10f, r);
     const float s = r * r;
     float u = 2.6083159809786593541503e-06f;
     u = fmaf(u, s, -0.0001981069071916863322258f);
     u = fmaf(u, s, 0.00833307858556509017944336f);
     u = fmaf(u, s, -0.166666597127914428710938f);
-    float y = fmaf(s, u * r, r);
-    const int qi = (int)q;
-    return (qi & 1) ? -y : y;
+    const float y = fmaf(s, u * r, r);
+    const unsigned sgn = ((unsigned)(int)q & 1u) << 31;  // negate for odd q
+    const float v = __uint_as_float(__float_as_uint(y) ^ sgn);
+    return fabsf(x) < 39000.0f ? v : __builtin_amdgcn_sinf(x * 0.159154943091895335768f);
 }
 
 }  // namespace cfd

@@ -22,6 +22,7 @@
 //   * sin(w0*x) uses a Cody-Waite reduced polynomial (common.hpp sin_cw);
 //   * the last (H -> c) layer, the bias and the per-point de-normalisation are
 //     fused into the store.
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -77,8 +78,11 @@ __device__ __forceinline__ void siren_issue_block(const float* __restrict__ wimg
     }
 }
 
-template <int NB>
-__global__ __launch_bounds__(256, (NB <= 24 ? 2 : 1)) void siren_fused(SirenArgs p) {
+// DUAL = false: one accumulation chain per 16-row block, 2 workgroups per CU
+//              (256 VGPRs: the partner workgroup hides the MFMA dependency);
+// DUAL = true : two interleaved chains, 1 workgroup per CU (512 VGPRs).
+template <int NB, bool DUAL>
+__global__ __launch_bounds__(256, (NB <= 24 && !DUAL ? 2 : 1)) void siren_fused(SirenArgs p) {
     constexpr int H = NB * 16;
     constexpr int BLK = NB * 256;  // floats in one 16-row weight block image
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -122,18 +126,19 @@ __global__ __launch_bounds__(256, (NB <= 24 ? 2 : 1)) void siren_fused(SirenArgs
 
     // ---- layer 0: x = sin(w0 * (W0 c + F_0)) ----
     float X[NB][4];
+    auto layer0_arg = [&](int q, int r) -> float {
+        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
+        const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
+        float a = cn[0] * w[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+            if (k < p.d) a = fmaf(cn[k], w[k], a);
+        return p.w0f * (a + fv[r]);
+    };
     static_for<NB>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
-        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
-            float a = cn[0] * w[0];
-#pragma unroll
-            for (int k = 1; k < 4; ++k)
-                if (k < p.d) a = fmaf(cn[k], w[k], a);
-            X[q][r] = sin_cw(p.w0f * (a + fv[r]));
-        }
+        for (int r = 0; r < 4; ++r) X[q][r] = sin_cw(layer0_arg(q, r));
     });
 
     // ---- hidden layers on fp32 MFMA 16x16x4 ----
@@ -145,16 +150,31 @@ __global__ __launch_bounds__(256, (NB <= 24 ? 2 : 1)) void siren_fused(SirenArgs
             constexpr int j = decltype(jc)::value;
             if (J + 1 < nblocks) siren_issue_block<NB>(p.wimg, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
             const float* wb = wbuf + (J & 1) * BLK;
+            // two interleaved accumulation chains (even / odd k-steps): the f32
+            // 16x16x4 MFMA has a 40-cycle dependent latency vs a 32-cycle issue
             f4 a = *(const f4*)(film + layer * H + 16 * j + 4 * g);
-            static_for<NB>([&](auto qc) {
-                constexpr int q = decltype(qc)::value;
-                const f4 w = *(const f4*)(wb + (q * 64 + lane) * 4);
-                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, X[q][0], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, X[q][1], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, X[q][2], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, X[q][3], a, 0, 0, 0);
-            });
-            acc[j] = a;
+            if constexpr (DUAL) {
+                f4 a2 = {0.f, 0.f, 0.f, 0.f};
+                static_for<NB>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    const f4 w = *(const f4*)(wb + (q * 64 + lane) * 4);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, X[q][0], a, 0, 0, 0);
+                    a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, X[q][1], a2, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, X[q][2], a, 0, 0, 0);
+                    a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, X[q][3], a2, 0, 0, 0);
+                });
+                acc[j] = a + a2;
+            } else {
+                static_for<NB>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    const f4 w = *(const f4*)(wb + (q * 64 + lane) * 4);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, X[q][0], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, X[q][1], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, X[q][2], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, X[q][3], a, 0, 0, 0);
+                });
+                acc[j] = a;
+            }
             // block J+1 landed (this wave's pieces) -> barrier makes every wave's
             // pieces visible and retires all reads of slot J&1 before it is refilled.
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -239,17 +259,29 @@ struct cfd_siren {
 
 namespace {
 
+int siren_variant() {
+    static int v = [] {
+        const char* e = getenv("CFD_SIREN_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 template <int NB>
 void launch_siren_nb(const cfd_siren* h, cfd::SirenArgs a, int b, hipStream_t st) {
     const int H = NB * 16;
     const size_t lds = (size_t)(2 * NB * 256 + (h->cfg.num_hidden_layers + 1) * H + 4 * H) * sizeof(float);
-    CFD_HIP(hipFuncSetAttribute((const void*)cfd::siren_fused<NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
+    const bool dual = siren_variant() == 1;
+    const void* fn = dual ? (const void*)cfd::siren_fused<NB, true> : (const void*)cfd::siren_fused<NB, false>;
+    CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t tiles = cfd::ceil_div(a.N, cfd::SIREN_TILE);
     for (int64_t b0 = 0; b0 < b; b0 += 65535) {
         a.b0 = b0;
         const int nb = (int)std::min<int64_t>(65535, b - b0);
-        hipLaunchKernelGGL(cfd::siren_fused<NB>, dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
+        if (dual)
+            hipLaunchKernelGGL((cfd::siren_fused<NB, true>), dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
+        else
+            hipLaunchKernelGGL((cfd::siren_fused<NB, false>), dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
         cfd::check_launch("siren_fused");
     }
 }

@@ -243,11 +243,28 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         max_c2 = 2 * (size_t)std::max(ch, c.channel_mult[0] * mc) * 4;  // generous for concat stats
         for (int l = 0; l < c.n_mult; ++l) max_c2 = std::max(max_c2, (size_t)4 * c.channel_mult[l] * mc * 2);
     }
+    constexpr size_t kSplitCap = size_t(8) << 20;  // floats in the split-K partial slab
     float* temb = ws.take((size_t)B * mc);
     float* h1 = ws.take((size_t)B * h->tdim);
     float* emb = ws.take((size_t)B * h->tdim);
     float* embo = ws.take((size_t)B * h->emb_total);
-    float* ss = ws.take((size_t)B * max_c2);
+    (void)max_c2;
+    double* gnpart = (double*)ws.take((size_t)B * 64 * 32 * 2 * 2);
+    float* gnss = ws.take((size_t)B * 1024 * 2);
+    // normalised (+SiLU) input of the next conv; the widest is an output block's
+    // concat (current + skip channels) at its level: bound by hw^2 * (C_level + C_max)
+    size_t max_cat = 0;
+    {
+        int cmax = 0, hw = S;
+        for (int l = 0; l < c.n_mult; ++l) cmax = std::max(cmax, c.channel_mult[l] * mc);
+        for (int l = 0; l < c.n_mult; ++l) {
+            max_cat = std::max(max_cat, (size_t)hw * hw * (c.channel_mult[l] * mc + cmax));
+            if (l != c.n_mult - 1) hw /= 2;
+        }
+        max_cat = std::max(max_cat, max_act);
+    }
+    float* nbuf = ws.take((size_t)B * max_cat);
+    float* splitk = ws.take(kSplitCap);
     float* pool[3];
     for (auto& p : pool) p = ws.take((size_t)B * max_act);
     float* tmp = ws.take((size_t)B * max_act);
@@ -283,12 +300,26 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     cfd::launch_linear(h1, P(h, "time_embed.2.weight"), P(h, "time_embed.2.bias"), emb, B, h->tdim, h->tdim, 1, st);
     cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, st);
 
-    auto gn = [&](const Act& in, const std::string& pre) {
-        cfd::GnArgs g{in.a, in.b, P(h, pre + ".weight"), P(h, pre + ".bias"), ss, in.Ca, in.Cb, in.C(),
-                      in.H * in.W, 1e-5f};
-        cfd::launch_gn_stats(g, B, st);
+    // GroupNorm(+SiLU) of `in` materialised once into nbuf (contiguous Ctot channels)
+    auto gn = [&](const Act& in, const std::string& pre, int silu) -> Act {
+        cfd::GnArgs g{};
+        g.src1 = in.a;
+        g.src2 = in.b;
+        g.gamma = P(h, pre + ".weight");
+        g.beta = P(h, pre + ".bias");
+        g.part = gnpart;
+        g.ss = gnss;
+        g.out = nbuf;
+        g.C1 = in.Ca;
+        g.C2 = in.Cb;
+        g.Ctot = in.C();
+        g.HW = in.H * in.W;
+        g.eps = 1e-5f;
+        g.silu = silu;
+        cfd::launch_gn(g, B, st);
+        return Act{nbuf, in.C(), nullptr, 0, in.H, in.W};
     };
-    auto conv = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up, int act,
+    auto conv = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up,
                     const float* embp, const float* resp, float* out) {
         cfd::ConvArgs a{};
         a.src1 = in.a;
@@ -296,13 +327,13 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         a.C1 = in.Ca;
         a.C2 = in.Cb;
         a.Ctot = in.C();
-        a.ss = act ? ss : nullptr;
         a.w = P(h, pre + ".weight");
         a.bias = P(h, pre + ".bias");
         a.emb = embp;
         a.emb_stride = h->emb_total;
         a.res = resp;
         a.out = out;
+        a.part = splitk;
         a.Hin = in.H;
         a.Win = in.W;
         a.Hout = up ? in.H * 2 : (stride == 2 ? (in.H + 1) / 2 : in.H);
@@ -312,10 +343,9 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         a.pad = ks == 3 ? 1 : 0;
         a.up = up;
         a.Cout = cout;
-        a.act = act;
         a.M = B * a.Hout * a.Wout;
         a.K = ks * ks * a.Ctot;
-        cfd::launch_conv(a, st);
+        cfd::launch_conv(a, cfd::plan_conv(a, kSplitCap), st);
     };
 
     std::vector<Act> stack;
@@ -370,55 +400,54 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 const auto& r = h->res[s.idx];
                 CFD_REQUIRE(cur.C() == r.cin, CFD_ESTATE, "internal: ResBlock input channels at " + r.pre);
                 // h = in_layers(x) + emb_layers(emb)   (unet.py:236-254)
-                gn(cur, r.pre + ".in_layers.0");
-                conv(cur, r.pre + ".in_layers.2", r.cout, 3, 1, 0, 2, embo + r.emb_off, nullptr, tmp);
+                const Act xin = gn(cur, r.pre + ".in_layers.0", 1);
+                conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, tmp);
                 const Act th{tmp, r.cout, nullptr, 0, cur.H, cur.W};
                 // skip(x) + out_layers(h)   (unet.py:255-256)
                 const float* resp;
                 if (r.cin != r.cout) {
-                    conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, 0, nullptr, nullptr, skipb);
+                    conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
                     resp = skipb;
                 } else {
                     CFD_REQUIRE(cur.b == nullptr, CFD_ESTATE, "identity skip on a concatenated input");
                     resp = cur.a;
                 }
-                gn(th, r.pre + ".out_layers.0");
+                const Act hn = gn(th, r.pre + ".out_layers.0", 1);
                 float* out = dest(cur.a, cur.b);
-                conv(th, r.pre + ".out_layers.3", r.cout, 3, 1, 0, 2, nullptr, resp, out);
+                conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};
                 break;
             }
             case cfd::Step::Attn: {
                 const auto& at = h->attn[s.idx];
-                gn(cur, at.pre + ".norm");
-                conv(cur, at.pre + ".qkv", 3 * at.C, 1, 1, 0, 1, nullptr, nullptr, qkv);
+                const Act xn = gn(cur, at.pre + ".norm", 0);
+                conv(xn, at.pre + ".qkv", 3 * at.C, 1, 1, 0, nullptr, nullptr, qkv);
                 cfd::AttnArgs aa{qkv, abuf, cur.H * cur.W, at.C, (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
                 cfd::launch_attention(aa, at.ch, at.heads, B, st);
                 float* out = dest(cur.a, nullptr);
-                conv(Act{abuf, at.C, nullptr, 0, cur.H, cur.W}, at.pre + ".proj_out", at.C, 1, 1, 0, 0, nullptr,
-                     cur.a, out);
+                conv(Act{abuf, at.C, nullptr, 0, cur.H, cur.W}, at.pre + ".proj_out", at.C, 1, 1, 0, nullptr, cur.a,
+                     out);
                 cur = Act{out, at.C, nullptr, 0, cur.H, cur.W};
                 break;
             }
             case cfd::Step::Down: {
                 float* out = dest(cur.a, nullptr);
-                conv(cur, s.conv, s.cout, 3, 2, 0, 0, nullptr, nullptr, out);
+                conv(cur, s.conv, s.cout, 3, 2, 0, nullptr, nullptr, out);
                 cur = Act{out, s.cout, nullptr, 0, (cur.H + 1) / 2, (cur.W + 1) / 2};
                 break;
             }
             case cfd::Step::Up: {
                 float* out = pick(cur.a, nullptr);
-                conv(cur, s.conv, s.cout, 3, 1, 1, 0, nullptr, nullptr, out);
+                conv(cur, s.conv, s.cout, 3, 1, 1, nullptr, nullptr, out);
                 cur = Act{out, s.cout, nullptr, 0, cur.H * 2, cur.W * 2};
                 break;
             }
             case cfd::Step::Out: {
-                gn(cur, "out.0");
+                const Act on = gn(cur, "out.0", 1);
                 cfd::ConvArgs a{};
-                a.src1 = cur.a;
-                a.C1 = cur.Ca;
-                a.Ctot = cur.Ca;
-                a.ss = ss;
+                a.src1 = on.a;
+                a.C1 = on.Ca;
+                a.Ctot = on.Ca;
                 a.w = P(h, "out.2.weight");
                 a.bias = P(h, "out.2.bias");
                 a.out = eps;

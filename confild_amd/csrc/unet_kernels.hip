@@ -1,84 +1,148 @@
 // Latent U-Net kernels for gfx950 (K1-K5 of DESIGN.md), fp32, NHWC activations.
 //
 //   conv_gemm   K1/K2  implicit-GEMM 3x3 / 1x1 convolution on fp32 MFMA 16x16x4,
-//                      GroupNorm(+SiLU) applied while staging the input tile
-//                      (prologue), bias / timestep-embedding / residual fused in the
-//                      epilogue, concat-free two-source input (skip connections),
-//                      stride-2 (Downsample) and nearest-2x (Upsample) addressing;
-//   gn_stats    K3     GroupNorm(32) statistics -> per-(b,c) scale/shift;
+//                      bias / timestep-embedding / residual fused in the epilogue,
+//                      concat-free two-source input (skip connections), stride-2
+//                      (Downsample) and nearest-2x (Upsample) addressing, split-K
+//                      for the low-resolution levels;
+//   gn_partial/apply K3 GroupNorm(32) statistics + normalise (+SiLU), written once;
 //   attention   K4     QKVAttentionLegacy (flash-style, fp32 MFMA, online softmax);
 //   temb/linear K5     timestep embedding + time_embed MLP + all emb_layers;
 //   conv_in / conv_out the 1-channel first/last convolutions (VALU).
+#include <algorithm>
+#include <cstdlib>
+
 #include "unet_kernels.hpp"
 
 namespace cfd {
 
 // ---------------------------------------------------------------------------
-// K3: GroupNorm statistics.  One workgroup per (group, sample).  Output, per
-// (b, c): scale = rstd*gamma, shift = beta - mean*scale, so the consumer applies
-// y = x*scale + shift (the affine form of the ATen CPU GroupNorm kernel).
+// K3: GroupNorm(32), eps 1e-5, statistics in float64 (nn.py:17-19 computes GN
+// in fp32; double accumulation keeps the result within rounding of the exact
+// moments).  Two passes over the data:
+//   gn_partial  per (pixel chunk, sample): per-group sum and sum of squares of
+//               its pixels, read as coalesced full-channel rows (two sources =
+//               the concat-free skip input);
+//   gn_apply    per-(b, c) scale/shift from the partials (fixed summation order,
+//               deterministic), then y = x*scale + shift (+ SiLU) written as one
+//               contiguous (B, HW, Ctot) tensor for the next convolution.
 // ---------------------------------------------------------------------------
-__global__ void gn_stats_kernel(GnArgs a) {
-    const int grp = blockIdx.x;
+__global__ __launch_bounds__(256) void gn_partial_kernel(GnArgs a) {
+    const int chunk = blockIdx.x;
     const int64_t b = blockIdx.y;
-    const int cpg = a.Ctot / 32;
-    const int64_t n = (int64_t)a.HW * cpg;
-    const float* s1 = a.src1 + b * (int64_t)a.HW * a.C1;
-    const float* s2 = a.src2 ? a.src2 + b * (int64_t)a.HW * a.C2 : nullptr;
-    __shared__ double red[8];
-    __shared__ double bc_mean, bc_rstd;
-
-    auto load = [&](int64_t idx) -> float {
-        const int64_t p = idx / cpg;
-        const int c = grp * cpg + (int)(idx - p * cpg);
-        return c < a.C1 ? s1[p * a.C1 + c] : s2[p * a.C2 + (c - a.C1)];
-    };
-    auto block_sum = [&](double v) -> double {
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-        __syncthreads();
-        double t = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
-        __syncthreads();
-        return t;
-    };
-    double s = 0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += load(i);
-    const double mean = block_sum(s) / (double)n;
-    double v2 = 0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const double d = (double)load(i) - mean;
-        v2 += d * d;
-    }
-    const double var = block_sum(v2) / (double)n;
-    if (threadIdx.x == 0) {
-        bc_mean = mean;
-        bc_rstd = 1.0 / sqrt(var + (double)a.eps);
+    const int Ctot = a.Ctot, cq = Ctot / 4, cpg = Ctot / 32;
+    const int HW = a.HW;
+    const int p0 = (int)((int64_t)HW * chunk / a.nchunks), p1 = (int)((int64_t)HW * (chunk + 1) / a.nchunks);
+    // thread t owns channel quad q = t % cq for pixel rows r0 = t / cq (step `rows`);
+    // rows * cq <= 256 so rows * Ctot <= 1024 per-channel sums per block
+    const int rows = 256 / cq;
+    const int q = threadIdx.x % cq, r0 = threadIdx.x / cq;
+    __shared__ double red[2][1024];
+    if (r0 < rows) {
+        double s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+        const int c0 = 4 * q;
+        for (int p = p0 + r0; p < p1; p += rows) {
+            const int64_t pix = b * HW + p;
+            const f4 v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0)
+                                   : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s[j] += v[j];
+                s2[j] += (double)v[j] * v[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            red[0][r0 * Ctot + c0 + j] = s[j];
+            red[1][r0 * Ctot + c0 + j] = s2[j];
+        }
     }
     __syncthreads();
-    const float meanf = (float)bc_mean, rstd = (float)bc_rstd;
-    for (int j = threadIdx.x; j < cpg; j += blockDim.x) {
-        const int c = grp * cpg + j;
-        const float sc = rstd * a.gamma[c];
-        a.ss[(b * a.Ctot + c) * 2 + 0] = sc;
-        a.ss[(b * a.Ctot + c) * 2 + 1] = a.beta[c] - meanf * sc;
+    // one thread per group sums its channels over the rows in a fixed order
+    if (threadIdx.x < 32) {
+        const int grp = threadIdx.x;
+        double ts = 0, ts2 = 0;
+        for (int r = 0; r < rows; ++r)
+            for (int c = grp * cpg; c < (grp + 1) * cpg; ++c) {
+                ts += red[0][r * Ctot + c];
+                ts2 += red[1][r * Ctot + c];
+            }
+        double* dst = a.part + ((b * a.nchunks + chunk) * 32 + grp) * 2;
+        dst[0] = ts;
+        dst[1] = ts2;
     }
 }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
+// per (b, c): scale = rstd*gamma, shift = beta - mean*scale (ATen CPU GroupNorm
+// affine form) from the chunk partials, summed in a fixed order.
+__global__ __launch_bounds__(256) void gn_finalize_kernel(GnArgs a) {
+    const int64_t b = blockIdx.x;
+    const int Ctot = a.Ctot, cpg = Ctot / 32;
+    __shared__ float sh_mean[32], sh_rstd[32];
+    if (threadIdx.x < 32) {
+        const int grp = threadIdx.x;
+        double s = 0, s2 = 0;
+        for (int ch = 0; ch < a.nchunks; ++ch) {
+            const double* src = a.part + ((b * a.nchunks + ch) * 32 + grp) * 2;
+            s += src[0];
+            s2 += src[1];
+        }
+        const double n = (double)a.HW * cpg;
+        const double mean = s / n;
+        const double var = fmax(s2 / n - mean * mean, 0.0);
+        sh_mean[grp] = (float)mean;
+        sh_rstd[grp] = (float)(1.0 / sqrt(var + (double)a.eps));
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < Ctot; c += blockDim.x) {
+        const int grp = c / cpg;
+        const float sc = sh_rstd[grp] * a.gamma[c];
+        a.ss[(b * Ctot + c) * 2 + 0] = sc;
+        a.ss[(b * Ctot + c) * 2 + 1] = a.beta[c] - sh_mean[grp] * sc;
+    }
+}
+
+// y = x*scale + shift (+ SiLU), one float4 per thread, written as one
+// contiguous (B, HW, Ctot) tensor (the concat of two sources materialised here).
+__global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
+    const int cq = a.Ctot / 4;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)a.B * a.HW * cq) return;
+    const int64_t pix = i / cq;
+    const int c0 = (int)(i - pix * cq) * 4;
+    const int64_t b = pix / a.HW;
+    f4 v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0) : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
+    const float* ss = a.ss + (b * a.Ctot + c0) * 2;
+    const f4 s01 = *(const f4*)ss, s23 = *(const f4*)(ss + 4);
+    v[0] = v[0] * s01[0] + s01[1];
+    v[1] = v[1] * s01[2] + s01[3];
+    v[2] = v[2] * s23[0] + s23[1];
+    v[3] = v[3] * s23[2] + s23[3];
+    if (a.silu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
+    }
+    *(f4*)(a.out + pix * a.Ctot + c0) = v;
+}
+
 // ---------------------------------------------------------------------------
 // K1/K2: implicit-GEMM convolution.  GEMM view: M = B*Hout*Wout output pixels,
-// N = Cout, K = ks*ks*Ctot ordered (tap, channel).  Workgroup tile BM x BN x 16,
-// 4 waves as 2x2, each wave (BM/2)x(BN/2) built from 16x16 fp32 MFMA tiles.
-// LDS tiles are [row][16 + 4 pad]; lane (g = lane>>4, i = lane&15) reads one
-// ds_read_b128 per operand per 4 MFMA k-steps, with physical k = 4g + s.
+// N = Cout, K = ks*ks*Ctot ordered (tap, channel).  Workgroup tile BM x BN x 32,
+// 4 waves as 2x2, each wave (BM/2)x(BN/2) of 16x16 fp32 MFMA tiles.  LDS tiles
+// are [row][32 + 4 pad] (conflict-free ds_read_b128); lane group g = lane>>4
+// owns k in [8g, 8g+8) of every 32-deep tile (the same permutation for A and B).
+// Register-staged double buffer: tile k+1 is loaded while tile k is multiplied.
+// Optional split-K (gridDim.z > 1): partial sums go to a (split, M, N) slab and
+// splitk_reduce applies the epilogue.
 // ---------------------------------------------------------------------------
 template <int BM, int BN>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
-    constexpr int LDK = 20;
-    constexpr int TM = BM / 32, TN = BN / 32;
-    constexpr int AIT = BM / 64, BIT = BN / 64;
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
+    constexpr int BK = 32, LDK = 36;
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int TM = WM / 16, TN = WN / 16;
+    constexpr int AIT = BM / 32, BIT = BN / 32;  // float4 per thread per tile
     __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
@@ -86,14 +150,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     const int wm = wave >> 1, wn = wave & 1;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const int HWo = a.Hout * a.Wout;
-    const int kq = tid & 3;
+    const int kq = tid & 7, rsub = tid >> 3;  // 8 threads per 32-float row
 
-    // per-thread A rows (fixed over the K loop)
     int a_b[AIT], a_oy[AIT], a_ox[AIT];
     bool a_ok[AIT];
 #pragma unroll
     for (int it = 0; it < AIT; ++it) {
-        const int m = m0 + (tid >> 2) + it * 64;
+        const int m = m0 + rsub + it * 32;
         a_ok[it] = m < a.M;
         const int mm = a_ok[it] ? m : 0;
         a_b[it] = mm / HWo;
@@ -101,14 +164,17 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         a_oy[it] = rem / a.Wout;
         a_ox[it] = rem - a_oy[it] * a.Wout;
     }
-    const int nK = a.K / 16;
+    const int nkt = a.K / BK;
+    const int per = (nkt + gridDim.z - 1) / gridDim.z;
+    const int kt0 = blockIdx.z * per;
+    const int kt1 = min(nkt, kt0 + per);
 
     f4 ra[AIT], rb[BIT];
     auto load_tile = [&](int kt) {
-        const int kbase = kt * 16;
+        const int kbase = kt * BK;
         const int tap = kbase / a.Ctot;
         const int c0 = kbase - tap * a.Ctot + 4 * kq;
-        const int dy = tap / a.ks, dx = tap - (tap / a.ks) * a.ks;
+        const int dy = tap / a.ks, dx = tap - dy * a.ks;
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             f4 v = {0.f, 0.f, 0.f, 0.f};
@@ -128,32 +194,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
                 const int64_t pix = ((int64_t)a_b[it] * a.Hin + iy) * a.Win + ix;
                 v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0)
                               : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
-                if (a.act) {
-                    const float* ss = a.ss + ((int64_t)a_b[it] * a.Ctot + c0) * 2;
-                    const f4 s01 = *(const f4*)ss, s23 = *(const f4*)(ss + 4);
-                    v[0] = v[0] * s01[0] + s01[1];
-                    v[1] = v[1] * s01[2] + s01[3];
-                    v[2] = v[2] * s23[0] + s23[1];
-                    v[3] = v[3] * s23[2] + s23[3];
-                    if (a.act == 2) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
-                    }
-                }
             }
             ra[it] = v;
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
-            const int n = n0 + (tid >> 2) + it * 64;
+            const int n = n0 + rsub + it * 32;
             rb[it] = n < a.Cout ? *(const f4*)(a.w + (int64_t)n * a.K + kbase + 4 * kq) : f4{0.f, 0.f, 0.f, 0.f};
         }
     };
     auto store_tile = [&](int buf) {
 #pragma unroll
-        for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][((tid >> 2) + it * 64) * LDK + 4 * kq]) = ra[it];
+        for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][(rsub + it * 32) * LDK + 4 * kq]) = ra[it];
 #pragma unroll
-        for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][((tid >> 2) + it * 64) * LDK + 4 * kq]) = rb[it];
+        for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][(rsub + it * 32) * LDK + 4 * kq]) = rb[it];
     };
 
     f4 acc[TM][TN];
@@ -162,40 +216,64 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-    const int g4 = 4 * (lane >> 4), li = lane & 15;
-    for (int kt = 0; kt < nK; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nK) load_tile(kt + 1);
-        f4 fa[TM], fb[TN];
+    const int g8 = 8 * (lane >> 4), li = lane & 15;
+    if (kt0 < kt1) {
+        load_tile(kt0);
+        store_tile(0);
+        __syncthreads();
+        for (int kt = kt0; kt < kt1; ++kt) {
+            const int cur = (kt - kt0) & 1;
+            if (kt + 1 < kt1) load_tile(kt + 1);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *(const f4*)(&As[cur][(wm * (BM / 2) + 16 * i + li) * LDK + g4]);
+            for (int h = 0; h < 2; ++h) {
+                f4 fa[TM], fb[TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = *(const f4*)(&Bs[cur][(wn * (BN / 2) + 16 * j + li) * LDK + g4]);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
+                for (int i = 0; i < TM; ++i)
+                    fa[i] = *(const f4*)(&As[cur][(wm * WM + 16 * i + li) * LDK + g8 + 4 * h]);
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-        if (kt + 1 < nK) store_tile(cur ^ 1);
-        __syncthreads();
+                    fb[j] = *(const f4*)(&Bs[cur][(wn * WN + 16 * j + li) * LDK + g8 + 4 * h]);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+            }
+            if (kt + 1 < kt1) store_tile(cur ^ 1);
+            __syncthreads();
+        }
     }
 
-    // epilogue: + bias (+ emb[b, n]) then residual + h
+    const int g4 = 4 * (lane >> 4);
+    if (gridDim.z > 1) {
+        float* part = a.part + (int64_t)blockIdx.z * a.M * a.Cout;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * WM + 16 * i + g4 + r;
+                if (m >= a.M) continue;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wn * WN + 16 * j + li;
+                    if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][r];
+                }
+            }
+        return;
+    }
+    // epilogue: (acc + bias) (+ emb[b, n]); residual + h
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * (BM / 2) + 16 * i + g4 + r;
+            const int m = m0 + wm * WM + 16 * i + g4 + r;
             if (m >= a.M) continue;
             const int bb = m / HWo;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wn * (BN / 2) + 16 * j + li;
+                const int n = n0 + wn * WN + 16 * j + li;
                 if (n >= a.Cout) continue;
                 float v = acc[i][j][r] + a.bias[n];
                 if (a.emb) v = v + a.emb[(int64_t)bb * a.emb_stride + n];
@@ -204,6 +282,28 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
             }
         }
     }
+}
+
+// sum of split-K partials in split order + the conv epilogue
+__global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
+    const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total4 = (int64_t)a.M * a.Cout / 4;
+    if (i4 >= total4) return;
+    const int64_t i = i4 * 4;
+    f4 s = *(const f4*)(a.part + i);
+    for (int k = 1; k < splits; ++k) s += *(const f4*)(a.part + (int64_t)k * a.M * a.Cout + i);
+    const int64_t m = i / a.Cout;
+    const int n = (int)(i - m * a.Cout);
+    const int bb = (int)(m / (a.Hout * a.Wout));
+    f4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float y = s[j] + a.bias[n + j];
+        if (a.emb) y = y + a.emb[(int64_t)bb * a.emb_stride + n + j];
+        if (a.res) y = a.res[i + j] + y;
+        v[j] = y;
+    }
+    *(f4*)(a.out + i) = v;
 }
 
 // First convolution, in_channels (<= 4) -> Cout, 3x3 pad 1: VALU, one output per thread.
@@ -224,7 +324,7 @@ __global__ void conv_in_kernel(ConvArgs a) {
     a.out[idx] = s + a.bias[n];
 }
 
-// Last convolution: GN+SiLU prologue, Ctot -> Cout (<= 4), 3x3 pad 1.  One wave
+// Last convolution (input already GroupNorm+SiLU'd), Ctot -> Cout (<= 4), 3x3 pad 1.  One wave
 // per output pixel; lanes split K = 9*Ctot, wave-reduced.
 __global__ void conv_out_kernel(ConvArgs a) {
     const int lane = threadIdx.x & 63;
@@ -237,9 +337,7 @@ __global__ void conv_out_kernel(ConvArgs a) {
         const int tap = k / a.Ctot, c = k - tap * a.Ctot;
         const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
         if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
-        float v = a.src1[(((int64_t)b * a.Hin + iy) * a.Win + ix) * a.C1 + c];
-        const float* ss = a.ss + ((int64_t)b * a.Ctot + c) * 2;
-        v = silu_f(v * ss[0] + ss[1]);
+        const float v = a.src1[(((int64_t)b * a.Hin + iy) * a.Win + ix) * a.C1 + c];
         for (int n = 0; n < a.Cout; ++n) s[n] = fmaf(a.w[(int64_t)n * a.K + k], v, s[n]);
     }
     for (int n = 0; n < a.Cout; ++n) {
@@ -389,24 +487,66 @@ __global__ void linear_kernel(const float* __restrict__ x, const float* __restri
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-void launch_gn_stats(const GnArgs& a, int B, hipStream_t st) {
-    CFD_REQUIRE(a.Ctot % 32 == 0, CFD_ESHAPE, "GroupNorm32 needs channels % 32 == 0");
-    hipLaunchKernelGGL(gn_stats_kernel, dim3(32, B), dim3(256), 0, st, a);
-    check_launch("gn_stats_kernel");
+int gn_chunks(int HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 16)); }
+
+void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
+    CFD_REQUIRE(a0.Ctot % 32 == 0 && a0.C1 % 4 == 0 && a0.C2 % 4 == 0 && a0.Ctot <= 1024, CFD_ESHAPE,
+                "GroupNorm32 needs channels % 32 == 0 (<= 1024)");
+    GnArgs a = a0;
+    a.nchunks = gn_chunks(a.HW);
+    a.B = B;
+    hipLaunchKernelGGL(gn_partial_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
+    check_launch("gn_partial_kernel");
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(256), 0, st, a);
+    check_launch("gn_finalize_kernel");
+    const int64_t nq = (int64_t)B * a.HW * a.Ctot / 4;
+    hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a);
+    check_launch("gn_apply_kernel");
 }
 
-void launch_conv(const ConvArgs& a, hipStream_t st) {
-    CFD_REQUIRE(a.Ctot % 16 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 16 == 0");
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
+    // tuning knobs (development): CFD_CONV_BM (0 = auto, 64, 128), CFD_CONV_TARGET_WG
+    static const int force_bm = env_int("CFD_CONV_BM", 0);
+    static const int target = env_int("CFD_CONV_TARGET_WG", 512);
+    ConvPlan p;
+    p.bn = a.Cout >= 128 ? 128 : 64;
+    auto tiles = [&](int bm) { return ceil_div(a.M, bm) * ceil_div(a.Cout, p.bn); };
+    if (force_bm)
+        p.bm = force_bm;
+    else
+        p.bm = tiles(128) < target ? 64 : 128;
+    const int nkt = a.K / 32;
+    p.splits = 1;
+    while (tiles(p.bm) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16 &&
+           (size_t)(p.splits * 2) * a.M * a.Cout <= part_cap_floats)
+        p.splits *= 2;
+    return p;
+}
+
+void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
+    CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
     CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot, CFD_ESHAPE, "conv K mismatch");
-    const int64_t t128 = ceil_div(a.M, 128) * ceil_div(a.Cout, 128);
-    if (t128 >= 256 && a.Cout % 128 == 0) {
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 128>), dim3((unsigned)ceil_div(a.M, 128), (unsigned)ceil_div(a.Cout, 128)),
-                           dim3(256), 0, st, a);
-    } else {
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 64>), dim3((unsigned)ceil_div(a.M, 64), (unsigned)ceil_div(a.Cout, 64)),
-                           dim3(256), 0, st, a);
-    }
+    CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
+    const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
+    if (p.bm == 128 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 128>), grid, dim3(256), 0, st, a);
+    else if (p.bm == 64 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 128>), grid, dim3(256), 0, st, a);
+    else if (p.bm == 128 && p.bn == 64)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 64>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 64>), grid, dim3(256), 0, st, a);
     check_launch("conv_gemm_kernel");
+    if (p.splits > 1) {
+        const int64_t total4 = (int64_t)a.M * a.Cout / 4;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0, st, a, p.splits);
+        check_launch("splitk_reduce_kernel");
+    }
 }
 
 void launch_conv_in(const ConvArgs& a, hipStream_t st) {

@@ -1,0 +1,81 @@
+"""Kernel-level timing of the HIP path with HIP events (development tool).
+
+    python tools/kbench.py siren [--latents 64]      # config-B CNF decode
+    python tools/kbench.py unet  [--batch 8]         # one U-Net forward
+    python tools/kbench.py sweep                      # both, short
+Prints one JSON line per measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from confild_amd import synth  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def timeit(fn, iters=5, warm=1):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2], ts[0]
+
+
+def bench_siren(latents=64, npts=64 ** 3, dims=(3, 64, 3, 15, 384), iters=3):
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    d, L, c, nh, H = dims
+    net = SIRENAutodecoder_film(d, L, c, nh, H)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, d, L, c, nh, H).items()})
+    net.to(DEV)
+    coords = torch.rand(npts, d, device=DEV)
+    lat = torch.randn(latents, 1, L, device=DEV) * 0.5
+    med, best = timeit(lambda: net(coords, lat), iters=iters)
+    flops = latents * npts * 2 * (d * H + nh * H * H + H * c)
+    print(json.dumps({"kernel": "siren", "variant": os.environ.get("CFD_SIREN_VARIANT", "0"), "dims": dims,
+                      "latents": latents, "npts": npts, "ms": med, "best_ms": best,
+                      "tflops": flops / (best / 1e3) / 1e12}), flush=True)
+
+
+def bench_unet(batch=8, size=64, iters=10):
+    from confild_amd.script_util import create_model
+    m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                     attention_resolutions="32,16,8")
+    sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.to(DEV)
+    x = torch.randn(batch, 1, size, size, device=DEV)
+    t = torch.full((batch,), 500, dtype=torch.int64, device=DEV)
+    med, best = timeit(lambda: m(x, t), iters=iters, warm=2)
+    gf = {32: 19.23, 64: 68.61, 128: 140.75}.get(size, float("nan"))
+    print(json.dumps({"kernel": "unet_forward", "batch": batch, "size": size, "ms": med, "best_ms": best,
+                      "tflops": batch * gf * 1e9 / (best / 1e3) / 1e12}), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["siren", "unet", "sweep"])
+    ap.add_argument("--latents", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--size", type=int, default=64)
+    a = ap.parse_args()
+    if a.what in ("siren", "sweep"):
+        bench_siren(a.latents)
+    if a.what in ("unet", "sweep"):
+        bench_unet(a.batch, a.size)
