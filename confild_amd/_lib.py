@@ -53,8 +53,9 @@ _SIGS = {
     "cfd_sched_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "cfd_sched_destroy": (None, [C.c_void_p]),
     "cfd_sched_step": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                 C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p]),
-    "cfd_randn": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_void_p]),
+                                 C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int64, C.c_int,
+                                 C.c_void_p]),
+    "cfd_randn": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]),
     "cfd_latent_denorm": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                     C.c_void_p]),
     "cfd_siren_create": (C.c_int, [C.POINTER(SirenCfg), C.c_int, C.POINTER(C.c_void_p)]),

@@ -52,12 +52,12 @@ struct Philox {
     }
 };
 
-__global__ void randn_kernel(float* __restrict__ out, int64_t n, uint64_t seed, uint64_t counter) {
+__global__ void randn_kernel(float* __restrict__ out, int64_t n, uint64_t seed, uint64_t counter, uint64_t goff) {
     const int64_t grp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t base = grp * 4;
     if (base >= n) return;
     float z[4];
-    Philox::normal4(seed, counter, (uint64_t)grp, z);
+    Philox::normal4(seed, counter, goff + (uint64_t)grp, z);
     if (base + 3 < n) {
         *(f4*)(out + base) = f4{z[0], z[1], z[2], z[3]};  // out 16-B aligned when n % 4 == 0 (checked by caller)
     } else {
@@ -75,7 +75,7 @@ struct StepArgs {
     float* xs_out;       // may be null
     int64_t n;           // elements per sample
     int64_t total;       // B * n
-    uint64_t seed, counter;
+    uint64_t seed, counter, goff;  // goff: Philox group offset (= element offset / 4)
     int kind, clip;
 };
 
@@ -89,7 +89,7 @@ __global__ void step_kernel(StepArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) z[j] = (base + j < a.total) ? a.noise[base + j] : 0.f;
     } else {
-        Philox::normal4(a.seed, a.counter, (uint64_t)grp, z);
+        Philox::normal4(a.seed, a.counter, a.goff + (uint64_t)grp, z);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -157,14 +157,15 @@ extern "C" void cfd_sched_destroy(cfd_sched* s) {
 }
 
 extern "C" int cfd_sched_step(const cfd_sched* s, int kind, int clip, const float* x, const float* eps,
-                              const int64_t* t, const float* noise, uint64_t seed, uint64_t counter, float* x_out,
-                              float* xstart_out, int64_t n_per_sample, int B, void* stream) {
+                              const int64_t* t, const float* noise, uint64_t seed, uint64_t counter, uint64_t offset,
+                              float* x_out, float* xstart_out, int64_t n_per_sample, int B, void* stream) {
     return cfd::guard([&] {
         CFD_REQUIRE(s && x && eps && t && x_out, CFD_EARG, "null argument");
+        CFD_REQUIRE(offset % 4 == 0, CFD_EARG, "noise offset must be a multiple of 4");
         CFD_REQUIRE(kind == CFD_STEP_DDPM || kind == CFD_STEP_DDIM, CFD_EARG, "unknown step kind");
         CFD_REQUIRE(n_per_sample > 0 && B > 0, CFD_EARG, "empty step");
         cfd::StepArgs a{s->coefs, x, eps, t, noise, x_out, xstart_out, n_per_sample, n_per_sample * B,
-                        seed, counter, kind, clip};
+                        seed, counter, offset / 4, kind, clip};
         const int64_t groups = cfd::ceil_div(a.total, 4);
         hipLaunchKernelGGL(cfd::step_kernel, dim3((unsigned)cfd::ceil_div(groups, 256)), dim3(256), 0,
                            (hipStream_t)stream, a);
@@ -172,13 +173,14 @@ extern "C" int cfd_sched_step(const cfd_sched* s, int kind, int clip, const floa
     });
 }
 
-extern "C" int cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, void* stream) {
+extern "C" int cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, uint64_t offset, void* stream) {
     return cfd::guard([&] {
         CFD_REQUIRE(out && n > 0, CFD_EARG, "bad argument");
+        CFD_REQUIRE(offset % 4 == 0, CFD_EARG, "noise offset must be a multiple of 4");
         CFD_REQUIRE(((uintptr_t)out & 15) == 0, CFD_EARG, "randn output must be 16-byte aligned");
         const int64_t groups = cfd::ceil_div(n, 4);
         hipLaunchKernelGGL(cfd::randn_kernel, dim3((unsigned)cfd::ceil_div(groups, 256)), dim3(256), 0,
-                           (hipStream_t)stream, out, n, seed, counter);
+                           (hipStream_t)stream, out, n, seed, counter, offset / 4);
         cfd::check_launch("randn_kernel");
     });
 }

@@ -243,7 +243,9 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         max_c2 = 2 * (size_t)std::max(ch, c.channel_mult[0] * mc) * 4;  // generous for concat stats
         for (int l = 0; l < c.n_mult; ++l) max_c2 = std::max(max_c2, (size_t)4 * c.channel_mult[l] * mc * 2);
     }
-    constexpr size_t kSplitCap = size_t(8) << 20;  // floats in the split-K partial slab
+    // split-K partial slab: the plan needs at most 16 x (8 samples' M x N) at the
+    // low-resolution levels; scale with the batch so the memory guard never trips
+    const size_t kSplitCap = (size_t(8) << 20) * (size_t)std::max(1, (B + 7) / 8);
     float* temb = ws.take((size_t)B * mc);
     float* h1 = ws.take((size_t)B * h->tdim);
     float* emb = ws.take((size_t)B * h->tdim);

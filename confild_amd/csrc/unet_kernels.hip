@@ -515,16 +515,20 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     static const int target = env_int("CFD_CONV_TARGET_WG", 512);
     ConvPlan p;
     p.bn = a.Cout >= 128 ? 128 : 64;
-    auto tiles = [&](int bm) { return ceil_div(a.M, bm) * ceil_div(a.Cout, p.bn); };
+    auto tiles = [&](int64_t M, int bm) { return ceil_div(M, bm) * ceil_div(a.Cout, p.bn); };
     if (force_bm)
         p.bm = force_bm;
     else
-        p.bm = tiles(128) < target ? 64 : 128;
+        p.bm = tiles(a.M, 128) < target ? 64 : 128;
+    // The split-K count fixes the summation order of every output, so it is
+    // chosen from the per-sample shape (as if the batch were 8), never from the
+    // actual batch: a sample's eps is then bit-identical whatever batch (or
+    // rank shard) it is computed in.
+    const int64_t m_nominal = (int64_t)8 * a.Hout * a.Wout;
     const int nkt = a.K / 32;
     p.splits = 1;
-    while (tiles(p.bm) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16 &&
-           (size_t)(p.splits * 2) * a.M * a.Cout <= part_cap_floats)
-        p.splits *= 2;
+    while (tiles(m_nominal, 64) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16) p.splits *= 2;
+    while (p.splits > 1 && (size_t)p.splits * a.M * a.Cout > part_cap_floats) p.splits /= 2;  // memory guard
     return p;
 }
 

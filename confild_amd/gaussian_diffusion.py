@@ -164,7 +164,8 @@ class GaussianDiffusion:
         if self.model_mean_type != ModelMeanType.EPSILON:
             raise NotImplementedError(f"model_mean_type {self.model_mean_type} on the HIP path (CoNFiLD uses EPSILON)")
 
-    def _step(self, kind, model, x, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, noise, seed, counter, eta):
+    def _step(self, kind, model, x, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, noise, seed, counter, eta,
+              offset=0):
         self._check_mean_type()
         if denoised_fn is not None or cond_fn is not None:
             raise NotImplementedError("denoised_fn / cond_fn (use the DPS sampler for conditioning)")
@@ -184,7 +185,7 @@ class GaussianDiffusion:
         sched = self._sched(x.device, eta)
         n = x[0].numel()
         _lib.check(_lib.load().cfd_sched_step(sched.handle, kind, 1 if clip_denoised else 0, _lib.ptr(x),
-                                              _lib.ptr(eps), _lib.ptr(t), _lib.ptr(nz), seed, counter,
+                                              _lib.ptr(eps), _lib.ptr(t), _lib.ptr(nz), seed, counter, offset,
                                               _lib.ptr(out), _lib.ptr(xs), n, x.shape[0],
                                               _lib.stream_of(x.device)), "cfd_sched_step")
         return {"sample": out, "pred_xstart": xs}
@@ -207,7 +208,7 @@ class GaussianDiffusion:
 
     # -- loops ------------------------------------------------------------------
     def _loop(self, kind, model, shape, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs, device,
-              progress, eta, step_noise, seed):
+              progress, eta, step_noise, seed, sample_offset=0):
         if device is None:
             try:
                 device = next(model.parameters()).device
@@ -220,11 +221,15 @@ class GaussianDiffusion:
         lib = _lib.lib()
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        per_sample = int(np.prod(shape[1:]))
+        offset = sample_offset * per_sample   # Philox position of this shard's first element
+        if offset % 4:
+            raise ValueError("sharded sampling needs (elements per sample * first sample) % 4 == 0")
         if noise is not None:
             img = noise.to(device=device, dtype=torch.float32).contiguous()
         else:
             img = torch.empty(*shape, dtype=torch.float32, device=device)
-            _lib.check(lib.cfd_randn(_lib.ptr(img), img.numel(), seed, 1 << 40, _lib.stream_of(device)),
+            _lib.check(lib.cfd_randn(_lib.ptr(img), img.numel(), seed, 1 << 40, offset, _lib.stream_of(device)),
                        "cfd_randn")
         indices = list(range(self.num_timesteps))[::-1]
         if progress:
@@ -237,38 +242,41 @@ class GaussianDiffusion:
             nz = None if step_noise is None else step_noise[k]
             with torch.no_grad():
                 out = self._step(kind, model, img, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, nz,
-                                 seed, k, eta)
+                                 seed, k, eta, offset)
             yield out
             img = out["sample"]
 
     def p_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
-                      model_kwargs=None, device=None, progress=False, step_noise=None, seed=None):
-        """gaussian_diffusion.py:441-485."""
+                      model_kwargs=None, device=None, progress=False, step_noise=None, seed=None, sample_offset=0):
+        """gaussian_diffusion.py:441-485.  ``sample_offset``: index of this call's first
+        sample in a larger (sharded) batch, so the Philox noise equals the unsharded run's."""
         final = None
         for s in self.p_sample_loop_progressive(model, shape, noise, clip_denoised, denoised_fn, cond_fn,
-                                                model_kwargs, device, progress, step_noise, seed):
+                                                model_kwargs, device, progress, step_noise, seed, sample_offset):
             final = s
         return final["sample"]
 
     def p_sample_loop_progressive(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None,
                                   cond_fn=None, model_kwargs=None, device=None, progress=False, step_noise=None,
-                                  seed=None):
+                                  seed=None, sample_offset=0):
         """gaussian_diffusion.py:487-535."""
         yield from self._loop(STEP_DDPM, model, shape, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
-                              device, progress, 0.0, step_noise, seed)
+                              device, progress, 0.0, step_noise, seed, sample_offset)
 
     def ddim_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
-                         model_kwargs=None, device=None, progress=False, eta=0.0, step_noise=None, seed=None):
+                         model_kwargs=None, device=None, progress=False, eta=0.0, step_noise=None, seed=None,
+                         sample_offset=0):
         """gaussian_diffusion.py:625-662."""
         final = None
         for s in self.ddim_sample_loop_progressive(model, shape, noise, clip_denoised, denoised_fn, cond_fn,
-                                                   model_kwargs, device, progress, eta, step_noise, seed):
+                                                   model_kwargs, device, progress, eta, step_noise, seed,
+                                                   sample_offset):
             final = s
         return final["sample"]
 
     def ddim_sample_loop_progressive(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None,
                                      cond_fn=None, model_kwargs=None, device=None, progress=False, eta=0.0,
-                                     step_noise=None, seed=None):
+                                     step_noise=None, seed=None, sample_offset=0):
         """gaussian_diffusion.py:664-707."""
         yield from self._loop(STEP_DDIM, model, shape, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
-                              device, progress, eta, step_noise, seed)
+                              device, progress, eta, step_noise, seed, sample_offset)

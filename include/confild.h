@@ -93,14 +93,18 @@ int  cfd_sched_create(const float* host_coefs, int n_t, int device, cfd_sched** 
 void cfd_sched_destroy(cfd_sched* s);
 /* x_out = step(x, eps, t).  t: (B) int64 device indices into the table.
  * noise: (B*n) device normals in the reference's draw order, or NULL to draw
- * them in-kernel with Philox4x32-10 keyed by (seed, counter).
+ * them in-kernel with Philox4x32-10 keyed by (seed, counter); element i of
+ * this call uses stream position offset + i (offset % 4 == 0), so a batch
+ * sharded over ranks draws exactly the normals of the unsharded batch.
  * xstart_out may be NULL.  x_out may alias x. */
 int  cfd_sched_step(const cfd_sched* s, int kind, int clip, const float* x, const float* eps,
                     const int64_t* t, const float* noise, uint64_t seed, uint64_t counter,
-                    float* x_out, float* xstart_out, int64_t n_per_sample, int B, void* stream);
-/* (B*n) standard normals from Philox4x32-10 (seed, counter): the device-side
- * stand-in for th.randn (gaussian_diffusion.py:513). */
-int  cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, void* stream);
+                    uint64_t offset, float* x_out, float* xstart_out, int64_t n_per_sample, int B,
+                    void* stream);
+/* n standard normals from Philox4x32-10 (seed, counter) at stream positions
+ * offset .. offset+n-1 (offset % 4 == 0): the device-side stand-in for th.randn
+ * (gaussian_diffusion.py:513). */
+int  cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, uint64_t offset, void* stream);
 /* Latent de-normalisation (scripts/inference.py:59-61): y = (x+1)*(max-min)/2 + min,
  * max/min broadcast over the trailing `period` elements (period=1: scalars). */
 int  cfd_latent_denorm(const float* x, float* y, int64_t n, const float* vmax, const float* vmin,

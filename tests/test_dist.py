@@ -1,0 +1,121 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the sharding and collective
+code in confild_amd.dist.  The compute is the CPU oracle, plugged in through the
+same callables the GPU path uses; the GPU path itself is the HIP decode."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from confild_amd import dist as cdist
+from confild_amd import synth
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    return out
+
+
+def _siren_decode_fn():
+    from oracle import siren as osn
+    d, L, c, nh, H = 3, 16, 3, 2, 32
+    sd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(3, d, L, c, nh, H).items()}
+
+    def fn(coords, latents, ymax, ymin):
+        return osn.decode(sd, coords, latents, torch.ones(1, d), torch.zeros(1, d), ymax, ymin)
+    return fn
+
+
+def _case_sharded_decode(rank, world):
+    N, b = 1001, 5
+    coords = torch.from_numpy(synth.uniform(1, "c", (N, 3), 0.0, 1.0))
+    lat = torch.from_numpy(synth.normal(2, "z", (b, 16)))
+    ymax = torch.from_numpy(synth.uniform(3, "ymax", (1, N, 3), 0.5, 2.0))
+    ymin = -ymax
+    fn = _siren_decode_fn()
+    full = cdist.sharded_decode(fn, coords, lat, ymax, ymin)
+    ref = fn(coords, lat, ymax, ymin)
+    return bool(torch.equal(full, ref)), tuple(full.shape)
+
+
+def _case_sharded_samples(rank, world):
+    B = 7
+
+    def sample_fn(start, count):  # deterministic per global sample index
+        return torch.stack([torch.full((4, 4), float(start + i)) for i in range(count)])
+    full = cdist.sharded_samples(sample_fn, B)
+    return [float(v) for v in full[:, 0, 0]]
+
+
+def _case_broadcast(rank, world):
+    torch.manual_seed(100 + rank)  # different init per rank
+    m = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.Linear(8, 3))
+    cdist.broadcast_module(m, src=0)
+    return [float(p.sum()) for p in m.parameters()]
+
+
+def _case_gather(rank, world):
+    N = 9
+    s, e = cdist.shard_range(N, rank, world)
+    x = torch.arange(s, e, dtype=torch.float32)[None].repeat(2, 1)
+    sizes = [cdist.shard_range(N, r, world)[1] - cdist.shard_range(N, r, world)[0] for r in range(world)]
+    out = cdist.gather_cat(x, 1, sizes, dst=0)
+    return None if out is None else out[0].tolist()
+
+
+def test_shard_range_covers_exactly():
+    for n in (1, 7, 64, 1000):
+        for g in (1, 2, 3, 8):
+            spans = [cdist.shard_range(n, r, g) for r in range(g)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(g - 1))
+
+
+def test_coordinate_sharded_decode_equals_unsharded():
+    out = _run(_case_sharded_decode)
+    assert out[0] == (True, (5, 1001, 3)) and out[1] == (True, (5, 1001, 3)), out
+
+
+def test_sample_sharding_preserves_global_order():
+    out = _run(_case_sharded_samples)
+    assert out[0] == out[1] == [float(i) for i in range(7)]
+
+
+def test_bucketed_weight_broadcast():
+    out = _run(_case_broadcast)
+    assert out[0] == out[1]
+
+
+def test_gather_to_root_uneven():
+    out = _run(_case_gather)
+    assert out[0] == [float(i) for i in range(9)] and out[1] is None

@@ -99,13 +99,18 @@ def test_device_rng_is_normal_and_deterministic(hip):
     a = torch.empty(1 << 20, device=DEV)
     b = torch.empty(1 << 20, device=DEV)
     for buf in (a, b):
-        _lib.check(lib.cfd_randn(_lib.ptr(buf), buf.numel(), 1234, 7, None), "randn")
+        _lib.check(lib.cfd_randn(_lib.ptr(buf), buf.numel(), 1234, 7, 0, None), "randn")
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert abs(a.mean().item()) < 5e-3 and abs(a.std().item() - 1) < 5e-3
-    _lib.check(lib.cfd_randn(_lib.ptr(b), b.numel(), 1234, 8, None), "randn")
+    _lib.check(lib.cfd_randn(_lib.ptr(b), b.numel(), 1234, 8, 0, None), "randn")
     torch.cuda.synchronize()
     assert not torch.equal(a, b)
+    # offset addressing: the second half drawn alone equals the second half of the whole
+    half = torch.empty(1 << 19, device=DEV)
+    _lib.check(lib.cfd_randn(_lib.ptr(half), half.numel(), 1234, 7, 1 << 19, None), "randn")
+    torch.cuda.synchronize()
+    assert torch.equal(half, a[1 << 19:])
 
 
 def test_latent_denorm_bitexact(hip):
