@@ -44,8 +44,8 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
 }
 
-constexpr int SIREN_WAVES = 4;
-constexpr int SIREN_TILE = 16 * SIREN_WAVES;  // coordinates per workgroup
+// coordinates per workgroup = 16 * waves (4 waves: 2 workgroups per CU; 8 waves:
+// one workgroup per CU, each LDS-DMA'd weight block shared by 128 coordinates)
 
 struct SirenArgs {
     const float* w0;      // (H, d)            net1.0.weight
@@ -66,12 +66,12 @@ struct SirenArgs {
     float w0f;
 };
 
-template <int NB>
+template <int NB, int WAVES>
 __device__ __forceinline__ void siren_issue_block(const float* __restrict__ wimg, int J, float* dst,
                                                   int wave, int lane) {
     constexpr int BLK = NB * 256;
     const float* src = wimg + (int64_t)J * BLK;
-    for (int piece = wave; piece < NB; piece += SIREN_WAVES) {
+    for (int piece = wave; piece < NB; piece += WAVES) {
         __builtin_amdgcn_global_load_lds((const void*)(src + piece * 256 + lane * 4),
                                          (__attribute__((address_space(3))) void*)(dst + piece * 256),
                                          16, 0, 0);
@@ -81,8 +81,10 @@ __device__ __forceinline__ void siren_issue_block(const float* __restrict__ wimg
 // DUAL = false: one accumulation chain per 16-row block, 2 workgroups per CU
 //              (256 VGPRs: the partner workgroup hides the MFMA dependency);
 // DUAL = true : two interleaved chains, 1 workgroup per CU (512 VGPRs).
-template <int NB, bool DUAL>
-__global__ __launch_bounds__(256, (NB <= 24 && !DUAL ? 2 : 1)) void siren_fused(SirenArgs p) {
+template <int NB, bool DUAL, int WAVES>
+// 2 waves per SIMD (256 VGPRs each) in both geometries; dual / NB 32: 1 wave per SIMD
+__global__ __launch_bounds__(64 * WAVES, (NB <= 24 && !DUAL) ? 2 : 1) void siren_fused(SirenArgs p) {
+    constexpr int TILE = 16 * WAVES;
     constexpr int H = NB * 16;
     constexpr int BLK = NB * 256;  // floats in one 16-row weight block image
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256, (NB <= 24 && !DUAL ? 2 : 1)) void siren_fused(
     const int g = lane >> 4;
     const int j16 = lane & 15;
     const int64_t b = p.b0 + blockIdx.y;
-    const int64_t n = (int64_t)blockIdx.x * SIREN_TILE + wave * 16 + j16;
+    const int64_t n = (int64_t)blockIdx.x * TILE + wave * 16 + j16;
     const int64_t nc = n < p.N ? n : p.N - 1;
     const int nh = p.nh;
 
@@ -102,11 +104,11 @@ __global__ __launch_bounds__(256, (NB <= 24 && !DUAL ? 2 : 1)) void siren_fused(
     {
         const float* fsrc = p.film + b * (int64_t)(nh + 1) * H;
         const int nf = (nh + 1) * H;
-        for (int i = threadIdx.x * 4; i < nf; i += 256 * 4) *(f4*)(film + i) = *(const f4*)(fsrc + i);
+        for (int i = threadIdx.x * 4; i < nf; i += 64 * WAVES * 4) *(f4*)(film + i) = *(const f4*)(fsrc + i);
     }
     // ---- layer-0 inputs: normalised coordinates; (H, d) weight staged as (H, 4) ----
     float* w0s = film + (nh + 1) * H;
-    for (int f = threadIdx.x; f < H; f += 256) {
+    for (int f = threadIdx.x; f < H; f += 64 * WAVES) {
         f4 w = {0.f, 0.f, 0.f, 0.f};
         for (int k = 0; k < p.d; ++k) w[k] = p.w0[f * p.d + k];
         *(f4*)(w0s + 4 * f) = w;
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(256, (NB <= 24 && !DUAL ? 2 : 1)) void siren_fused(
     }
 
     __syncthreads();  // film + w0 visible; every ordinary global load above has been consumed
-    if (nh > 0) siren_issue_block<NB>(p.wimg, 0, wbuf, wave, lane);
+    if (nh > 0) siren_issue_block<NB, WAVES>(p.wimg, 0, wbuf, wave, lane);
 
     // ---- layer 0: x = sin(w0 * (W0 c + F_0)) ----
     float X[NB][4];
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(256, (NB <= 24 && !DUAL ? 2 : 1)) void siren_fused(
         f4 acc[NB];
         static_for<NB>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            if (J + 1 < nblocks) siren_issue_block<NB>(p.wimg, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            if (J + 1 < nblocks) siren_issue_block<NB, WAVES>(p.wimg, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
             const float* wb = wbuf + (J & 1) * BLK;
             // two interleaved accumulation chains (even / odd k-steps): the f32
             // 16x16x4 MFMA has a 40-cycle dependent latency vs a 32-cycle issue
@@ -262,7 +264,7 @@ namespace {
 int siren_variant() {
     static int v = [] {
         const char* e = getenv("CFD_SIREN_VARIANT");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 2;
     }();
     return v;
 }
@@ -271,17 +273,23 @@ template <int NB>
 void launch_siren_nb(const cfd_siren* h, cfd::SirenArgs a, int b, hipStream_t st) {
     const int H = NB * 16;
     const size_t lds = (size_t)(2 * NB * 256 + (h->cfg.num_hidden_layers + 1) * H + 4 * H) * sizeof(float);
-    const bool dual = siren_variant() == 1;
-    const void* fn = dual ? (const void*)cfd::siren_fused<NB, true> : (const void*)cfd::siren_fused<NB, false>;
+    const int v = siren_variant();  // 2 (default): 8 waves/WG, 0: 4 waves/WG, 1: dual chain
+    const void* fn = v == 1 ? (const void*)cfd::siren_fused<NB, true, 4>
+                   : v == 2 ? (const void*)cfd::siren_fused<NB, false, 8>
+                            : (const void*)cfd::siren_fused<NB, false, 4>;
     CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const int64_t tiles = cfd::ceil_div(a.N, cfd::SIREN_TILE);
+    const int waves = v == 2 ? 8 : 4;
+    const int64_t tiles = cfd::ceil_div(a.N, 16 * waves);
     for (int64_t b0 = 0; b0 < b; b0 += 65535) {
         a.b0 = b0;
         const int nb = (int)std::min<int64_t>(65535, b - b0);
-        if (dual)
-            hipLaunchKernelGGL((cfd::siren_fused<NB, true>), dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
+        const dim3 grid((unsigned)tiles, nb);
+        if (v == 1)
+            hipLaunchKernelGGL((cfd::siren_fused<NB, true, 4>), grid, dim3(256), lds, st, a);
+        else if (v == 2)
+            hipLaunchKernelGGL((cfd::siren_fused<NB, false, 8>), grid, dim3(512), lds, st, a);
         else
-            hipLaunchKernelGGL((cfd::siren_fused<NB, false>), dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
+            hipLaunchKernelGGL((cfd::siren_fused<NB, false, 4>), grid, dim3(256), lds, st, a);
         cfd::check_launch("siren_fused");
     }
 }

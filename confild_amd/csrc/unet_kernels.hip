@@ -130,21 +130,26 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
 // ---------------------------------------------------------------------------
 // K1/K2: implicit-GEMM convolution.  GEMM view: M = B*Hout*Wout output pixels,
 // N = Cout, K = ks*ks*Ctot ordered (tap, channel).  Workgroup tile BM x BN x 32,
-// 4 waves as 2x2, each wave (BM/2)x(BN/2) of 16x16 fp32 MFMA tiles.  LDS tiles
-// are [row][32 + 4 pad] (conflict-free ds_read_b128); lane group g = lane>>4
-// owns k in [8g, 8g+8) of every 32-deep tile (the same permutation for A and B).
-// Register-staged double buffer: tile k+1 is loaded while tile k is multiplied.
+// 4 waves as 2x2, each wave (BM/2)x(BN/2) of 16x16 fp32 MFMA tiles.
+// LDS tiles are [row][32 floats] with the 16-byte chunk index XOR-swizzled by
+// (row ^ row>>1) & 7: conflict-free for every ds_read_b128 lane group of the
+// fragment reads and for the ds_write_b128 staging (found by exhaustive check).
+// Lane group g = lane>>4 owns k in [8g, 8g+8) of every 32-deep tile (the same
+// permutation for A and B).  The (tap, channel) position advances incrementally
+// (no integer division in the K loop).  Register-staged double buffer.
 // Optional split-K (gridDim.z > 1): partial sums go to a (split, M, N) slab and
 // splitk_reduce applies the epilogue.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 32 + 4 * (chunk ^ ((row ^ (row >> 1)) & 7)); }
+
 template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
-    constexpr int BK = 32, LDK = 36;
+    constexpr int BK = 32;
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 16, TN = WN / 16;
     constexpr int AIT = BM / 32, BIT = BN / 32;  // float4 per thread per tile
-    __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
+    __shared__ __attribute__((aligned(16))) float As[2][BM * BK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * BK];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -163,31 +168,49 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         const int rem = mm - a_b[it] * HWo;
         a_oy[it] = rem / a.Wout;
         a_ox[it] = rem - a_oy[it] * a.Wout;
+        if (!a.up) {
+            a_oy[it] = a_oy[it] * a.stride - a.pad;
+            a_ox[it] = a_ox[it] * a.stride - a.pad;
+        } else {
+            a_oy[it] -= a.pad;
+            a_ox[it] -= a.pad;
+        }
+    }
+    const float* wrow[BIT];
+    bool b_ok[BIT];
+#pragma unroll
+    for (int it = 0; it < BIT; ++it) {
+        const int n = n0 + rsub + it * 32;
+        b_ok[it] = n < a.Cout;
+        wrow[it] = a.w + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
     }
     const int nkt = a.K / BK;
     const int per = (nkt + gridDim.z - 1) / gridDim.z;
     const int kt0 = blockIdx.z * per;
     const int kt1 = min(nkt, kt0 + per);
+    // wave-uniform K position: (dy, dx) tap and channel base, advanced per tile
+    int cb = 0, dy = 0, dx = 0;
+    {
+        const int kb = kt0 * BK;
+        const int tap = kb / a.Ctot;
+        cb = kb - tap * a.Ctot;
+        dy = tap / a.ks;
+        dx = tap - dy * a.ks;
+    }
 
     f4 ra[AIT], rb[BIT];
     auto load_tile = [&](int kt) {
-        const int kbase = kt * BK;
-        const int tap = kbase / a.Ctot;
-        const int c0 = kbase - tap * a.Ctot + 4 * kq;
-        const int dy = tap / a.ks, dx = tap - dy * a.ks;
+        const int c0 = cb + 4 * kq;
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             f4 v = {0.f, 0.f, 0.f, 0.f};
-            int iy, ix;
+            int iy = a_oy[it] + dy, ix = a_ox[it] + dx;
             bool ok = a_ok[it];
             if (a.up) {
-                const int iyu = a_oy[it] + dy - a.pad, ixu = a_ox[it] + dx - a.pad;
-                ok = ok && iyu >= 0 && iyu < 2 * a.Hin && ixu >= 0 && ixu < 2 * a.Win;
-                iy = iyu >> 1;
-                ix = ixu >> 1;
+                ok = ok && iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                iy >>= 1;
+                ix >>= 1;
             } else {
-                iy = a_oy[it] * a.stride + dy - a.pad;
-                ix = a_ox[it] * a.stride + dx - a.pad;
                 ok = ok && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
             }
             if (ok) {
@@ -198,16 +221,22 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
             ra[it] = v;
         }
 #pragma unroll
-        for (int it = 0; it < BIT; ++it) {
-            const int n = n0 + rsub + it * 32;
-            rb[it] = n < a.Cout ? *(const f4*)(a.w + (int64_t)n * a.K + kbase + 4 * kq) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int it = 0; it < BIT; ++it)
+            rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kt * BK) : f4{0.f, 0.f, 0.f, 0.f};
+        cb += BK;
+        if (cb >= a.Ctot) {
+            cb = 0;
+            if (++dx == a.ks) {
+                dx = 0;
+                ++dy;
+            }
         }
     };
     auto store_tile = [&](int buf) {
 #pragma unroll
-        for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][(rsub + it * 32) * LDK + 4 * kq]) = ra[it];
+        for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][lds_swz(rsub + it * 32, kq)]) = ra[it];
 #pragma unroll
-        for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][(rsub + it * 32) * LDK + 4 * kq]) = rb[it];
+        for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][lds_swz(rsub + it * 32, kq)]) = rb[it];
     };
 
     f4 acc[TM][TN];
@@ -216,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-    const int g8 = 8 * (lane >> 4), li = lane & 15;
+    const int g2 = 2 * (lane >> 4), li = lane & 15;
     if (kt0 < kt1) {
         load_tile(kt0);
         store_tile(0);
@@ -228,11 +257,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
             for (int h = 0; h < 2; ++h) {
                 f4 fa[TM], fb[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    fa[i] = *(const f4*)(&As[cur][(wm * WM + 16 * i + li) * LDK + g8 + 4 * h]);
+                for (int i = 0; i < TM; ++i) fa[i] = *(const f4*)(&As[cur][lds_swz(wm * WM + 16 * i + li, g2 + h)]);
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    fb[j] = *(const f4*)(&Bs[cur][(wn * WN + 16 * j + li) * LDK + g8 + 4 * h]);
+                for (int j = 0; j < TN; ++j) fb[j] = *(const f4*)(&Bs[cur][lds_swz(wn * WN + 16 * j + li, g2 + h)]);
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -510,24 +537,21 @@ static int env_int(const char* name, int dflt) {
 }
 
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
-    // tuning knobs (development): CFD_CONV_BM (0 = auto, 64, 128), CFD_CONV_TARGET_WG
+    // Every choice is made from the per-sample shape (as if the batch were 8),
+    // never from the actual batch: the split-K count fixes each output's
+    // summation order, so a sample's eps is then bit-identical whatever batch
+    // (or rank shard) it is computed in.  Knobs (development): CFD_CONV_BM
+    // (0 = auto), CFD_CONV_TARGET_WG.
     static const int force_bm = env_int("CFD_CONV_BM", 0);
     static const int target = env_int("CFD_CONV_TARGET_WG", 512);
     ConvPlan p;
+    const int64_t mn = (int64_t)8 * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;
-    auto tiles = [&](int64_t M, int bm) { return ceil_div(M, bm) * ceil_div(a.Cout, p.bn); };
-    if (force_bm)
-        p.bm = force_bm;
-    else
-        p.bm = tiles(a.M, 128) < target ? 64 : 128;
-    // The split-K count fixes the summation order of every output, so it is
-    // chosen from the per-sample shape (as if the batch were 8), never from the
-    // actual batch: a sample's eps is then bit-identical whatever batch (or
-    // rank shard) it is computed in.
-    const int64_t m_nominal = (int64_t)8 * a.Hout * a.Wout;
+    auto tiles = [&](int bm) { return ceil_div(mn, bm) * ceil_div(a.Cout, p.bn); };
+    p.bm = force_bm ? force_bm : (p.bn == 128 ? 128 : 64);
     const int nkt = a.K / 32;
     p.splits = 1;
-    while (tiles(m_nominal, 64) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16) p.splits *= 2;
+    while (tiles(p.bm) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16) p.splits *= 2;
     while (p.splits > 1 && (size_t)p.splits * a.M * a.Cout > part_cap_floats) p.splits /= 2;  // memory guard
     return p;
 }
