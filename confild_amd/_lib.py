@@ -50,6 +50,12 @@ _SIGS = {
     "cfd_unet_workspace_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]),
     "cfd_unet_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                    C.c_size_t, C.c_void_p]),
+    "cfd_unet_tape_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]),
+    "cfd_unet_vjp_workspace_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]),
+    "cfd_unet_forward_tape": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                        C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "cfd_unet_input_vjp": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t,
+                                     C.c_void_p, C.c_size_t, C.c_void_p]),
     "cfd_sched_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "cfd_sched_destroy": (None, [C.c_void_p]),
     "cfd_sched_step": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -58,6 +64,13 @@ _SIGS = {
     "cfd_randn": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]),
     "cfd_latent_denorm": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                     C.c_void_p]),
+    "cfd_dps_residual": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int,
+                                   C.c_void_p]),
+    "cfd_dps_latent_grad": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.c_int,
+                                      C.c_void_p]),
+    "cfd_dps_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_int64,
+                                 C.c_void_p]),
     "cfd_siren_create": (C.c_int, [C.POINTER(SirenCfg), C.c_int, C.POINTER(C.c_void_p)]),
     "cfd_siren_destroy": (None, [C.c_void_p]),
     "cfd_siren_num_params": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
@@ -69,6 +82,12 @@ _SIGS = {
     "cfd_siren_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                     C.c_size_t, C.c_void_p]),
+    "cfd_siren_vjp_workspace_bytes": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_size_t)]),
+    "cfd_siren_tape_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                         C.c_size_t, C.c_void_p]),
+    "cfd_siren_tape_vjp": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
+                                     C.c_int64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -129,6 +129,69 @@ __global__ void latent_denorm_kernel(const float* __restrict__ x, float* __restr
     y[i] = (x[i] + 1.0f) * (vmax[k] - vmin[k]) / 2.0f + vmin[k];
 }
 
+// ---------------------------------------------------------------------------
+// DPS glue: the elementwise links of
+// d||y - A(x0_hat)|| / d x_t that are not the U-Net or SIREN adjoints.
+// ---------------------------------------------------------------------------
+// per sample b: r = y - A, norm_b = ||r||_2 (float64 sum), g_A = -r / norm_b
+// (torch.linalg.norm backward; zero gradient where the norm is 0), condition_methods.py:33-35
+__global__ __launch_bounds__(256) void dps_residual_kernel(const float* __restrict__ y, int64_t y_bstride,
+                                                           const float* __restrict__ A, float* __restrict__ gA,
+                                                           float* __restrict__ norm, int64_t n) {
+    const int64_t b = blockIdx.x;
+    const float* yb = y + b * y_bstride;
+    const float* Ab = A + b * n;
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float r = yb[i] - Ab[i];
+        s += (double)r * r;
+    }
+    __shared__ double red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    const float nb = (float)sqrt(red[0]);
+    if (threadIdx.x == 0) norm[b] = nb;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float r = yb[i] - Ab[i];
+        gA[b * n + i] = nb > 0.f ? -(r / nb) : 0.f;
+    }
+}
+
+// g_z -> (d_eps, g_direct) through Case4Operator._unnorm (measurements.py:219-220),
+// clamp(-1, 1) (posterior_mean_variance.py:40-45; gradient passes on the closed
+// interval) and x0 = sra * x - srm1 * eps (:120-123)
+__global__ void dps_latent_grad_kernel(const float* __restrict__ coefs, int clip, const float* __restrict__ x,
+                                       const float* __restrict__ eps, const int64_t* __restrict__ t,
+                                       const float* __restrict__ gz, const float* __restrict__ vmax,
+                                       const float* __restrict__ vmin, int64_t period, float* __restrict__ d_eps,
+                                       float* __restrict__ g_direct, int64_t n, int64_t total) {
+#pragma clang fp contract(off)
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t b = i / n, k = i % period;
+    const float* c = coefs + t[b] * CFD_NCOEF;
+    const float x0u = c[CFD_COEF_SRA] * x[i] - c[CFD_COEF_SRM1] * eps[i];
+    const bool pass = !clip || (x0u >= -1.0f && x0u <= 1.0f);
+    const float gx0 = (gz[i] / 2.0f) * (vmax[k] - vmin[k]);
+    const float g = pass ? gx0 : 0.0f;
+    d_eps[i] = -g * c[CFD_COEF_SRM1];
+    g_direct[i] = g * c[CFD_COEF_SRA];
+}
+
+// x_t -= (d/dx_prev) * scale   (condition_methods.py:88)
+__global__ void dps_update_kernel(const float* __restrict__ sample, const float* __restrict__ g_direct,
+                                  const float* __restrict__ g_unet, float scale, float* __restrict__ x_out,
+                                  int64_t n) {
+#pragma clang fp contract(off)
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    x_out[i] = sample[i] - (g_direct[i] + g_unet[i]) * scale;
+}
+
 }  // namespace cfd
 
 struct cfd_sched {
@@ -192,5 +255,42 @@ extern "C" int cfd_latent_denorm(const float* x, float* y, int64_t n, const floa
         hipLaunchKernelGGL(cfd::latent_denorm_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0,
                            (hipStream_t)stream, x, y, n, vmax, vmin, period);
         cfd::check_launch("latent_denorm_kernel");
+    });
+}
+
+extern "C" int cfd_dps_residual(const float* y, int64_t y_batch_stride, const float* A, float* g_A, float* norm,
+                                int64_t n_per_sample, int B, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(y && A && g_A && norm && n_per_sample > 0 && B > 0, CFD_EARG, "bad argument");
+        CFD_REQUIRE(y_batch_stride == 0 || y_batch_stride == n_per_sample, CFD_EARG,
+                    "measurement must be shared (stride 0) or per sample (stride n)");
+        hipLaunchKernelGGL(cfd::dps_residual_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, y, y_batch_stride, A,
+                           g_A, norm, n_per_sample);
+        cfd::check_launch("dps_residual_kernel");
+    });
+}
+
+extern "C" int cfd_dps_latent_grad(const cfd_sched* s, int clip, const float* x, const float* eps, const int64_t* t,
+                                   const float* g_z, const float* vmax, const float* vmin, int64_t period,
+                                   float* d_eps, float* g_direct, int64_t n_per_sample, int B, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(s && x && eps && t && g_z && vmax && vmin && d_eps && g_direct, CFD_EARG, "null argument");
+        CFD_REQUIRE(n_per_sample > 0 && B > 0 && period > 0 && n_per_sample % period == 0, CFD_EARG,
+                    "latent bounds must tile the latent");
+        const int64_t total = n_per_sample * B;
+        hipLaunchKernelGGL(cfd::dps_latent_grad_kernel, dim3((unsigned)cfd::ceil_div(total, 256)), dim3(256), 0,
+                           (hipStream_t)stream, s->coefs, clip, x, eps, t, g_z, vmax, vmin, period, d_eps, g_direct,
+                           n_per_sample, total);
+        cfd::check_launch("dps_latent_grad_kernel");
+    });
+}
+
+extern "C" int cfd_dps_update(const float* sample, const float* g_direct, const float* g_unet, float scale,
+                              float* x_out, int64_t n, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(sample && g_direct && g_unet && x_out && n > 0, CFD_EARG, "bad argument");
+        hipLaunchKernelGGL(cfd::dps_update_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0,
+                           (hipStream_t)stream, sample, g_direct, g_unet, scale, x_out, n);
+        cfd::check_launch("dps_update_kernel");
     });
 }

@@ -236,6 +236,182 @@ __global__ void siren_film(const float* __restrict__ V, const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Input-gradient (DPS adjoint): d<g, A(z)>/dz for the
+// Case4 measurement operator A = y_norm.denormalize(SIREN(x_norm(sensors), z))
+// (measurements.py:219-226).  One workgroup per latent row z, all sensors of the
+// row in groups of VJP_SG; thread j owns hidden feature j.  Sensor counts are
+// small (10 in the Case4 notebook), so this is VALU work on L2-resident weights:
+//   siren_tape_fwd  u_i = W_i x_i + F_i kept for every layer (the tape), x_{i+1} =
+//                   sin(w0 u_i); outputs A (coalesced W^T reads, x broadcast from LDS);
+//   siren_tape_vjp  delta_i = (W_{i+1}^T delta_{i+1}) * w0 cos(w0 u_i), summed over
+//                   sensors per layer, then g_z = sum_i V_i^T (sum_s delta_i).
+// ---------------------------------------------------------------------------
+constexpr int VJP_SG = 8;
+
+struct SirenVjpArgs {
+    const float* w0;     // (H, d)
+    const float* wtr;    // (nh, H, H) hidden weights transposed: wtr[i][k][j] = W_{i+1}[j][k]
+    const float* wraw;   // (nh, H, H) hidden weights as stored: W_{i+1}[j][k]
+    const float* wout;   // (c, H)
+    const float* bout;   // (c)
+    const float* V;      // (nh+1, H, L)
+    const float* film;   // (R, nh+1, H)
+    const float* coords; // (Ns, d) raw sensor coordinates
+    const float* xmax;
+    const float* xmin;
+    const float* ymax;
+    const float* ymin;
+    float* pre;          // (R, Ns, nh+1, H) tape
+    float* out;          // (R, Ns, c)  forward output A
+    const float* gout;   // (R, Ns, c)  gradient w.r.t. A
+    float* gz;           // (R, L)
+    int64_t ystride;
+    int Ns, d, c, nh, H, L;
+    float w0f;
+};
+
+__global__ __launch_bounds__(512) void siren_tape_fwd(SirenVjpArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // VJP_SG x H
+    const int64_t r = blockIdx.x;
+    const int j = threadIdx.x;
+    const int H = p.H, nl = p.nh + 1;
+    const float* film = p.film + r * nl * H;
+    for (int s0 = 0; s0 < p.Ns; s0 += VJP_SG) {
+        const int ns = min(VJP_SG, p.Ns - s0);
+        float* pre = p.pre + ((r * p.Ns + s0) * nl) * (int64_t)H;
+        if (j < H) {
+            const float f0 = film[j];
+#pragma unroll
+            for (int s = 0; s < VJP_SG; ++s) {
+                if (s < ns) {
+                    float a = 0.f;
+                    for (int k = 0; k < p.d; ++k) {
+                        float v = p.coords[(int64_t)(s0 + s) * p.d + k];
+                        if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+                        a = k == 0 ? v * p.w0[j * p.d] : fmaf(v, p.w0[j * p.d + k], a);
+                    }
+                    const float u = a + f0;
+                    pre[(int64_t)s * nl * H + j] = u;
+                    xs[s * H + j] = sin_cw(p.w0f * u);
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = 1; i <= p.nh; ++i) {
+            float acc[VJP_SG];
+            if (j < H) {
+                const float fi = film[i * H + j];
+#pragma unroll
+                for (int s = 0; s < VJP_SG; ++s) acc[s] = fi;
+                const float* wt = p.wtr + (int64_t)(i - 1) * H * H + j;
+                for (int k = 0; k < H; ++k) {
+                    const float w = wt[(int64_t)k * H];
+#pragma unroll
+                    for (int s = 0; s < VJP_SG; ++s)
+                        if (s < ns) acc[s] = fmaf(w, xs[s * H + k], acc[s]);
+                }
+            }
+            __syncthreads();
+            if (j < H) {
+#pragma unroll
+                for (int s = 0; s < VJP_SG; ++s) {
+                    if (s < ns) {
+                        pre[((int64_t)s * nl + i) * H + j] = acc[s];
+                        xs[s * H + j] = sin_cw(p.w0f * acc[s]);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (j < ns * p.c) {
+            const int s = j / p.c, oc = j - s * p.c;
+            float o = 0.f;
+            for (int k = 0; k < H; ++k) o = fmaf(p.wout[oc * H + k], xs[s * H + k], o);
+            o += p.bout[oc];
+            if (p.ymax) {
+                const int64_t yi = (int64_t)(s0 + s) * p.ystride + oc;
+                o = (o + 1.0f) / 2.0f * (p.ymax[yi] - p.ymin[yi]) + p.ymin[yi];
+            }
+            p.out[(r * p.Ns + s0 + s) * p.c + oc] = o;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(512) void siren_tape_vjp(SirenVjpArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int64_t r = blockIdx.x;
+    const int j = threadIdx.x;
+    const int H = p.H, nl = p.nh + 1;
+    float* dl = sm;                   // VJP_SG x H: this layer's deltas
+    float* dacc = sm + VJP_SG * H;    // nl x H: deltas summed over sensors
+    for (int i = j; i < nl * H; i += blockDim.x) dacc[i] = 0.f;
+    for (int s0 = 0; s0 < p.Ns; s0 += VJP_SG) {
+        const int ns = min(VJP_SG, p.Ns - s0);
+        const float* pre = p.pre + ((r * p.Ns + s0) * nl) * (int64_t)H;
+        // gradient w.r.t. the last hidden activation: W_out^T (g * dA/dout)
+        float gx[VJP_SG];
+#pragma unroll
+        for (int s = 0; s < VJP_SG; ++s) gx[s] = 0.f;
+        if (j < H) {
+#pragma unroll
+            for (int s = 0; s < VJP_SG; ++s) {
+                if (s < ns) {
+                    float a = 0.f;
+                    for (int oc = 0; oc < p.c; ++oc) {
+                        float gy = p.gout[(r * p.Ns + s0 + s) * p.c + oc];
+                        if (p.ymax) {
+                            const int64_t yi = (int64_t)(s0 + s) * p.ystride + oc;
+                            gy = gy * ((p.ymax[yi] - p.ymin[yi]) / 2.0f);
+                        }
+                        a = fmaf(p.wout[oc * H + j], gy, a);
+                    }
+                    gx[s] = a;
+                }
+            }
+        }
+        for (int i = p.nh; i >= 0; --i) {
+            if (j < H) {
+                float sum = 0.f;
+#pragma unroll
+                for (int s = 0; s < VJP_SG; ++s) {
+                    if (s < ns) {
+                        const float u = pre[((int64_t)s * nl + i) * H + j];
+                        const float dlt = gx[s] * (p.w0f * cosf(p.w0f * u));
+                        dl[s * H + j] = dlt;
+                        sum += dlt;
+                    }
+                }
+                dacc[i * H + j] += sum;
+            }
+            __syncthreads();
+            if (i > 0 && j < H) {
+                // gx = W_i^T delta_i  (W_i = hidden layer i, stored at slot i-1)
+#pragma unroll
+                for (int s = 0; s < VJP_SG; ++s) gx[s] = 0.f;
+                const float* w = p.wraw + (int64_t)(i - 1) * H * H + j;
+                for (int k = 0; k < H; ++k) {
+                    const float wv = w[(int64_t)k * H];
+#pragma unroll
+                    for (int s = 0; s < VJP_SG; ++s)
+                        if (s < ns) gx[s] = fmaf(wv, dl[s * H + k], gx[s]);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // g_z[l] = sum_i sum_f V_i[f][l] dacc[i][f]
+    for (int l = j; l < p.L; l += blockDim.x) {
+        float a = 0.f;
+        for (int i = 0; i < nl; ++i) {
+            const float* v = p.V + (int64_t)i * H * p.L + l;
+            for (int f = 0; f < H; ++f) a = fmaf(v[(int64_t)f * p.L], dacc[i * H + f], a);
+        }
+        p.gz[r * p.L + l] = a;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // handle
 // ---------------------------------------------------------------------------
 struct SirenParam {
@@ -257,6 +433,8 @@ struct cfd_siren {
     float* wimg = nullptr;  // nh * NB * NB*256
     float* wout = nullptr;  // (c, H)
     float* bout = nullptr;  // (c)
+    float* wraw = nullptr;  // (nh, H, H) hidden weights (input-gradient path)
+    float* wtr = nullptr;   // (nh, H, H) hidden weights transposed
 };
 
 namespace {
@@ -343,6 +521,8 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_HIP(hipMalloc(&h->wimg, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wout, sizeof(float) * c * H));
         CFD_HIP(hipMalloc(&h->bout, sizeof(float) * 4));
+        CFD_HIP(hipMalloc(&h->wraw, sizeof(float) * (size_t)std::max(nh, 1) * H * H));
+        CFD_HIP(hipMalloc(&h->wtr, sizeof(float) * (size_t)std::max(nh, 1) * H * H));
         *out = h;
     });
 }
@@ -355,6 +535,8 @@ extern "C" void cfd_siren_destroy(cfd_siren* h) {
     (void)hipFree(h->wimg);
     (void)hipFree(h->wout);
     (void)hipFree(h->bout);
+    (void)hipFree(h->wraw);
+    (void)hipFree(h->wtr);
     delete h;
 }
 
@@ -413,6 +595,11 @@ extern "C" int cfd_siren_set_param(cfd_siren* h, const char* key, const float* h
                                 host[(size_t)(16 * j + (lane & 15)) * H + 16 * q + 4 * (lane >> 4) + s];
             CFD_HIP(hipMemcpy(h->wimg + (size_t)(li - 1) * NB * NB * 256, img.data(), img.size() * 4,
                               hipMemcpyHostToDevice));
+            std::vector<float> tr((size_t)H * H);
+            for (int a = 0; a < H; ++a)
+                for (int bb = 0; bb < H; ++bb) tr[(size_t)bb * H + a] = host[(size_t)a * H + bb];
+            CFD_HIP(hipMemcpy(h->wraw + (size_t)(li - 1) * H * H, host, n * 4, hipMemcpyHostToDevice));
+            CFD_HIP(hipMemcpy(h->wtr + (size_t)(li - 1) * H * H, tr.data(), n * 4, hipMemcpyHostToDevice));
         }
         (void)c;
         prm->set = true;
@@ -469,5 +656,96 @@ extern "C" int cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, c
         a.nh = nh;
         a.w0f = h->cfg.w0;
         launch_siren(h, a, b, st);
+    });
+}
+
+namespace {
+
+void siren_vjp_args(const cfd_siren* h, cfd::SirenVjpArgs& a, int64_t Ns, int R, void* ws) {
+    const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features;
+    a.w0 = h->w0;
+    a.wtr = h->wtr;
+    a.wraw = h->wraw;
+    a.wout = h->wout;
+    a.bout = h->bout;
+    a.V = h->V;
+    a.film = (float*)ws;
+    a.pre = (float*)ws + (size_t)R * (nh + 1) * H;
+    a.Ns = (int)Ns;
+    a.d = h->cfg.in_coord_features;
+    a.c = h->cfg.out_features;
+    a.nh = nh;
+    a.H = H;
+    a.L = h->cfg.in_latent_features;
+    a.w0f = h->cfg.w0;
+}
+
+int vjp_threads(int H) { return (H + 63) / 64 * 64; }
+
+}  // namespace
+
+extern "C" int cfd_siren_vjp_workspace_bytes(const cfd_siren* h, int64_t Ns, int R, size_t* bytes) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && bytes && Ns >= 0 && R >= 0, CFD_EARG, "bad argument");
+        const size_t nl = h->cfg.num_hidden_layers + 1, H = h->cfg.hidden_features;
+        *bytes = sizeof(float) * ((size_t)R * nl * H + (size_t)R * Ns * nl * H);
+    });
+}
+
+extern "C" int cfd_siren_tape_forward(cfd_siren* h, const float* coords, int64_t Ns, const float* latents, int R,
+                                      const float* xmax, const float* xmin, const float* ymax, const float* ymin,
+                                      int64_t y_stride, float* out, void* ws, size_t ws_bytes, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && coords && latents && out && ws, CFD_EARG, "null argument");
+        CFD_REQUIRE(Ns >= 1 && Ns <= (1 << 20) && R >= 1, CFD_EARG, "bad sensor / row count");
+        CFD_REQUIRE((xmax == nullptr) == (xmin == nullptr) && (ymax == nullptr) == (ymin == nullptr), CFD_EARG,
+                    "normaliser bounds must be set in pairs");
+        size_t need = 0;
+        cfd_siren_vjp_workspace_bytes(h, Ns, R, &need);
+        CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
+        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features, L = h->cfg.in_latent_features;
+        auto st = (hipStream_t)stream;
+        cfd::SirenVjpArgs a{};
+        siren_vjp_args(h, a, Ns, R, ws);
+        a.coords = coords;
+        a.xmax = xmax;
+        a.xmin = xmin;
+        a.ymax = ymax;
+        a.ymin = ymin;
+        a.ystride = y_stride;
+        a.out = out;
+        hipLaunchKernelGGL(cfd::siren_film, dim3(nh + 1, R), dim3(128), 0, st, h->V, h->fbias, latents, (float*)ws,
+                           H, L, nh + 1);
+        cfd::check_launch("siren_film");
+        hipLaunchKernelGGL(cfd::siren_tape_fwd, dim3(R), dim3(vjp_threads(H)), sizeof(float) * cfd::VJP_SG * H, st,
+                           a);
+        cfd::check_launch("siren_tape_fwd");
+    });
+}
+
+extern "C" int cfd_siren_tape_vjp(cfd_siren* h, const float* g_out, int64_t Ns, int R, const float* ymax,
+                                  const float* ymin, int64_t y_stride, float* g_latents, void* ws, size_t ws_bytes,
+                                  void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && g_out && g_latents && ws, CFD_EARG, "null argument");
+        CFD_REQUIRE(Ns >= 1 && R >= 1, CFD_EARG, "bad sensor / row count");
+        CFD_REQUIRE((ymax == nullptr) == (ymin == nullptr), CFD_EARG, "ymax/ymin must both be set or both NULL");
+        size_t need = 0;
+        cfd_siren_vjp_workspace_bytes(h, Ns, R, &need);
+        CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
+        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features;
+        cfd::SirenVjpArgs a{};
+        siren_vjp_args(h, a, Ns, R, ws);
+        a.ymax = ymax;
+        a.ymin = ymin;
+        a.ystride = y_stride;
+        a.gout = g_out;
+        a.gz = g_latents;
+        const size_t lds = sizeof(float) * ((size_t)cfd::VJP_SG * H + (size_t)(nh + 1) * H);
+        CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the input-gradient kernel");
+        CFD_HIP(hipFuncSetAttribute((const void*)cfd::siren_tape_vjp, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+        hipLaunchKernelGGL(cfd::siren_tape_vjp, dim3(R), dim3(vjp_threads(H)), lds, (hipStream_t)stream, a);
+        cfd::check_launch("siren_tape_vjp");
     });
 }

@@ -23,6 +23,8 @@ struct UParam {
     size_t count = 0;
     int emb_row = 0;     // EmbW/EmbB: first row in the concatenated emb matrix
     bool set = false;
+    int tpack = 0;       // input-gradient pack: 0 none, 1 transposed (Cin, taps, Cout), 2 upsample 4x4 (Cin, 16, Cout)
+    size_t toffset = 0;  // floats into the transposed arena
 };
 
 struct ResSpec {
@@ -59,6 +61,8 @@ struct cfd_unet {
     float* emb_w = nullptr; // (emb_total, tdim)
     float* emb_b = nullptr; // (emb_total)
     float* freqs = nullptr; // (mc/2) timestep-embedding frequencies
+    float* arena_t = nullptr; // transposed conv weights (input-gradient path)
+    size_t arena_t_floats = 0;
 };
 
 namespace {
@@ -77,11 +81,12 @@ void add_param(cfd_unet* h, const std::string& key, std::vector<int64_t> shape, 
     h->params.push_back(p);
 }
 
-void add_conv(cfd_unet* h, const std::string& pre, int cin, int cout, int k, bool conv1d = false) {
+void add_conv(cfd_unet* h, const std::string& pre, int cin, int cout, int k, bool conv1d = false, bool up = false) {
     if (conv1d)
         add_param(h, pre + ".weight", {cout, cin, 1}, Pack::Conv1);
     else
         add_param(h, pre + ".weight", {cout, cin, k, k}, k == 3 ? Pack::Conv3 : Pack::Conv1);
+    h->params.back().tpack = up ? 2 : 1;
     add_param(h, pre + ".bias", {cout}, Pack::Raw);
 }
 
@@ -176,7 +181,7 @@ void build(cfd_unet* h) {
             }
             if (level && i == c.num_res_blocks) {
                 const std::string up = pre + "." + std::to_string(j) + ".conv";
-                add_conv(h, up, ch, ch, 3);
+                add_conv(h, up, ch, ch, 3, false, true);
                 h->steps.push_back({cfd::Step::Up, 0, up, ch, ch});
                 ds /= 2;
             }
@@ -194,6 +199,19 @@ void build(cfd_unet* h) {
         off += (p.count + 3) & ~size_t(3);  // keep 16-B alignment
     }
     h->arena_floats = off;
+    size_t toff = 0;
+    for (auto& p : h->params) {
+        if (!p.tpack) continue;
+        p.toffset = toff;
+        toff += ((p.tpack == 2 ? p.count / 9 * 16 : p.count) + 3) & ~size_t(3);
+    }
+    h->arena_t_floats = toff;
+}
+
+const float* PT(const cfd_unet* h, const std::string& key) {
+    auto it = h->index.find(key);
+    CFD_REQUIRE(it != h->index.end() && h->params[it->second].tpack, CFD_EKEY, "internal: missing conv " + key);
+    return h->arena_t + h->params[it->second].toffset;
 }
 
 const float* P(const cfd_unet* h, const std::string& key) {
@@ -224,86 +242,119 @@ struct Workspace {
     }
 };
 
-// Executes (or, with ws.dry, sizes) one forward.
-void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B, Workspace& ws, hipStream_t st) {
+// What the input-gradient walk needs from one forward step.
+struct Rec {
+    Act in;                         // step input
+    const float* h1 = nullptr;      // Res: in_layers output (conv1 + bias + emb)
+    float *ss1 = nullptr, *st1 = nullptr;  // first GroupNorm: scale/shift, mean/rstd
+    float *ss2 = nullptr, *st2 = nullptr;  // Res: out_layers GroupNorm
+    float *qkv = nullptr, *o = nullptr, *lse = nullptr;  // Attn
+    int skip_hs = -1;               // Res on a concat: skip-stack index of the second source
+    int push_hs = -1;               // Push: skip-stack index
+};
+
+// Forward tape: every activation the input-gradient needs lives in its own
+// region of the tape (nothing is recycled); recs describes where.
+struct Tape {
+    Workspace* tws;
+    std::vector<Rec>* recs;
+};
+
+struct Sizes {
+    size_t max_act = 0, max_qkv = 0, max_cat = 0, max_att = 0;  // floats per sample
+    std::vector<size_t> hs;                                     // skip-stack tensors, floats per sample
+};
+
+Sizes sizes(const cfd_unet* h) {
     const auto& c = h->cfg;
     const int mc = c.model_channels, S = c.image_size;
-    // sizes: largest activation (any block output / ResBlock intermediate) and qkv
-    size_t max_act = 0, max_qkv = 0, max_c2 = 0;
-    {
-        int ch = c.channel_mult[0] * mc, hw = S;
-        max_act = std::max(max_act, (size_t)hw * hw * ch);
-        for (int l = 0; l < c.n_mult; ++l) {
-            const int co = c.channel_mult[l] * mc;
-            max_act = std::max(max_act, (size_t)hw * hw * std::max(co, ch));
-            max_qkv = std::max(max_qkv, (size_t)hw * hw * 3 * co);
-            if (l != c.n_mult - 1) hw /= 2;
-            ch = co;
+    Sizes z;
+    int ch = c.channel_mult[0] * mc, hw = S, cmax = 0;
+    z.max_act = (size_t)hw * hw * ch;
+    z.hs.push_back((size_t)hw * hw * ch);
+    for (int l = 0; l < c.n_mult; ++l) cmax = std::max(cmax, c.channel_mult[l] * mc);
+    for (int l = 0; l < c.n_mult; ++l) {
+        const int co = c.channel_mult[l] * mc;
+        z.max_act = std::max(z.max_act, (size_t)hw * hw * std::max(co, ch));
+        z.max_qkv = std::max(z.max_qkv, (size_t)hw * hw * 3 * co);
+        // normalised concat input of an output block: hw^2 * (C_level + C_max)
+        z.max_cat = std::max(z.max_cat, (size_t)hw * hw * (co + cmax));
+        z.max_att = std::max(z.max_att, (size_t)hw * hw * co);  // heads * T <= C * T
+        for (int r = 0; r < c.num_res_blocks; ++r) z.hs.push_back((size_t)hw * hw * co);
+        ch = co;
+        if (l != c.n_mult - 1) {
+            hw /= 2;
+            z.hs.push_back((size_t)hw * hw * ch);
         }
-        max_c2 = 2 * (size_t)std::max(ch, c.channel_mult[0] * mc) * 4;  // generous for concat stats
-        for (int l = 0; l < c.n_mult; ++l) max_c2 = std::max(max_c2, (size_t)4 * c.channel_mult[l] * mc * 2);
     }
-    // split-K partial slab: the plan needs at most 16 x (8 samples' M x N) at the
-    // low-resolution levels; scale with the batch so the memory guard never trips
-    const size_t kSplitCap = (size_t(8) << 20) * (size_t)std::max(1, (B + 7) / 8);
+    z.max_cat = std::max(z.max_cat, z.max_act);
+    return z;
+}
+
+// split-K partial slab: plan_conv keeps splits * (8 samples' M x N) within
+// kSplitPer8 floats, so a slab of ceil(B/8) of those always suffices
+constexpr size_t kSplitPer8 = size_t(16) << 20;
+size_t split_cap(int B) { return kSplitPer8 * (size_t)std::max(1, (B + 7) / 8); }
+
+cfd::ConvPlan plan_checked(const cfd::ConvArgs& a, size_t slab_floats) {
+    const cfd::ConvPlan p = cfd::plan_conv(a, kSplitPer8);
+    CFD_REQUIRE(p.splits == 1 || (size_t)p.splits * a.M * a.Cout <= slab_floats, CFD_ESTATE,
+                "internal: split-K slab too small");
+    return p;
+}
+
+// Executes (or, with ws.dry, sizes) one forward.  With a tape, the activations
+// the input-gradient needs are kept in the tape and described in tape->recs;
+// launch == false replays the walk to recover those pointers without running.
+void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B, Workspace& ws, hipStream_t st,
+         Tape* tape = nullptr, bool launch_req = true) {
+    const auto& c = h->cfg;
+    const int mc = c.model_channels, S = c.image_size;
+    const Sizes z = sizes(h);
+    const bool launch = launch_req && !ws.dry && !(tape && tape->tws->dry);
+    const size_t kSplitCap = split_cap(B);
     float* temb = ws.take((size_t)B * mc);
     float* h1 = ws.take((size_t)B * h->tdim);
     float* emb = ws.take((size_t)B * h->tdim);
     float* embo = ws.take((size_t)B * h->emb_total);
-    (void)max_c2;
     double* gnpart = (double*)ws.take((size_t)B * 64 * 32 * 2 * 2);
     float* gnss = ws.take((size_t)B * 1024 * 2);
-    // normalised (+SiLU) input of the next conv; the widest is an output block's
-    // concat (current + skip channels) at its level: bound by hw^2 * (C_level + C_max)
-    size_t max_cat = 0;
-    {
-        int cmax = 0, hw = S;
-        for (int l = 0; l < c.n_mult; ++l) cmax = std::max(cmax, c.channel_mult[l] * mc);
-        for (int l = 0; l < c.n_mult; ++l) {
-            max_cat = std::max(max_cat, (size_t)hw * hw * (c.channel_mult[l] * mc + cmax));
-            if (l != c.n_mult - 1) hw /= 2;
-        }
-        max_cat = std::max(max_cat, max_act);
-    }
-    float* nbuf = ws.take((size_t)B * max_cat);
+    // normalised (+SiLU) input of the next conv (widest: an output block's concat)
+    float* nbuf = ws.take((size_t)B * z.max_cat);
     float* splitk = ws.take(kSplitCap);
     float* pool[3];
-    for (auto& p : pool) p = ws.take((size_t)B * max_act);
-    float* tmp = ws.take((size_t)B * max_act);
-    float* skipb = ws.take((size_t)B * max_act);
-    float* qkv = ws.take((size_t)B * max_qkv);
-    float* abuf = ws.take((size_t)B * max_act);
-    // skip stack buffers (one per Push)
+    for (auto& p : pool) p = ws.take((size_t)B * z.max_act);
+    float* tmp = ws.take((size_t)B * z.max_act);
+    float* skipb = ws.take((size_t)B * z.max_act);
+    float* qkv = tape ? nullptr : ws.take((size_t)B * z.max_qkv);
+    float* abuf = tape ? nullptr : ws.take((size_t)B * z.max_act);
+    // skip stack buffers (one per Push); in the tape when recording
     std::vector<float*> hsbuf;
-    {
-        int ch = c.channel_mult[0] * mc, hw = S;
-        hsbuf.push_back(ws.take((size_t)B * hw * hw * ch));
-        for (int l = 0; l < c.n_mult; ++l) {
-            const int co = c.channel_mult[l] * mc;
-            for (int r = 0; r < c.num_res_blocks; ++r) hsbuf.push_back(ws.take((size_t)B * hw * hw * co));
-            ch = co;
-            if (l != c.n_mult - 1) {
-                hw /= 2;
-                hsbuf.push_back(ws.take((size_t)B * hw * hw * ch));
-            }
-        }
-    }
-    if (ws.dry) return;
+    for (size_t n : z.hs) hsbuf.push_back(tape ? tape->tws->take((size_t)B * n) : ws.take((size_t)B * n));
+    if (ws.dry && !tape) return;
+    auto keep = [&](size_t nfloats) -> float* { return tape->tws->take(nfloats); };
+    std::vector<Rec>* recs = tape ? tape->recs : nullptr;
+    if (recs) recs->assign(h->steps.size(), Rec{});
 
     auto pick = [&](const float* busy1, const float* busy2) -> float* {
+        if (!launch && (ws.dry || !busy1)) return pool[0];
         for (auto p : pool)
             if (p != busy1 && p != busy2) return p;
         throw cfd::Error{CFD_ESTATE, "internal: buffer pool exhausted"};
     };
 
     // timestep embedding + time_embed MLP + every ResBlock's emb_layers (nn.py:118-136, unet.py:648,199-205)
-    cfd::launch_temb(t, h->freqs, temb, mc, B, st);
-    cfd::launch_linear(temb, P(h, "time_embed.0.weight"), P(h, "time_embed.0.bias"), h1, B, mc, h->tdim, 0, st);
-    cfd::launch_linear(h1, P(h, "time_embed.2.weight"), P(h, "time_embed.2.bias"), emb, B, h->tdim, h->tdim, 1, st);
-    cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, st);
+    if (launch) {
+        cfd::launch_temb(t, h->freqs, temb, mc, B, st);
+        cfd::launch_linear(temb, P(h, "time_embed.0.weight"), P(h, "time_embed.0.bias"), h1, B, mc, h->tdim, 0, st);
+        cfd::launch_linear(h1, P(h, "time_embed.2.weight"), P(h, "time_embed.2.bias"), emb, B, h->tdim, h->tdim, 1,
+                           st);
+        cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, st);
+    }
 
-    // GroupNorm(+SiLU) of `in` materialised once into nbuf (contiguous Ctot channels)
-    auto gn = [&](const Act& in, const std::string& pre, int silu) -> Act {
+    // GroupNorm(+SiLU) of `in` materialised once into nbuf (contiguous Ctot channels);
+    // with a tape the scale/shift and group statistics are kept in *ss / *stats
+    auto gn = [&](const Act& in, const std::string& pre, int silu, float** ss, float** stats) -> Act {
         cfd::GnArgs g{};
         g.src1 = in.a;
         g.src2 = in.b;
@@ -311,6 +362,10 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         g.beta = P(h, pre + ".bias");
         g.part = gnpart;
         g.ss = gnss;
+        if (tape) {
+            *ss = g.ss = keep((size_t)B * in.C() * 2);
+            *stats = g.stats = keep((size_t)B * 64);
+        }
         g.out = nbuf;
         g.C1 = in.Ca;
         g.C2 = in.Cb;
@@ -318,7 +373,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         g.HW = in.H * in.W;
         g.eps = 1e-5f;
         g.silu = silu;
-        cfd::launch_gn(g, B, st);
+        if (launch) cfd::launch_gn(g, B, st);
         return Act{nbuf, in.C(), nullptr, 0, in.H, in.W};
     };
     auto conv = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up,
@@ -347,19 +402,23 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         a.Cout = cout;
         a.M = B * a.Hout * a.Wout;
         a.K = ks * ks * a.Ctot;
-        cfd::launch_conv(a, cfd::plan_conv(a, kSplitCap), st);
+        if (launch) cfd::launch_conv(a, plan_checked(a, kSplitCap), st);
     };
 
-    std::vector<Act> stack;
+    std::vector<std::pair<Act, int>> stack;  // (tensor, skip index)
     Act cur;
     size_t hs_i = 0;
+    int pending_skip = -1;
     for (size_t si = 0; si < h->steps.size(); ++si) {
         const auto& s = h->steps[si];
+        Rec rec;
+        rec.in = cur;
         // a block output that is pushed onto the skip stack is written straight
-        // into its skip buffer (no copy)
+        // into its skip buffer (no copy); with a tape every output is kept
         const bool to_skip = si + 1 < h->steps.size() && h->steps[si + 1].kind == cfd::Step::Push;
-        auto dest = [&](const float* busy1, const float* busy2) -> float* {
-            return to_skip ? hsbuf[hs_i] : pick(busy1, busy2);
+        auto dest = [&](const float* busy1, const float* busy2, size_t nfl) -> float* {
+            if (to_skip) return hsbuf[hs_i];
+            return tape ? keep(nfl) : pick(busy1, busy2);
         };
         switch (s.kind) {
             case cfd::Step::In: {
@@ -374,7 +433,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 a.Win = a.Wout = S;
                 a.Cout = s.cout;
                 a.M = B * S * S;
-                cfd::launch_conv_in(a, st);
+                if (launch) cfd::launch_conv_in(a, st);
                 cur = Act{hsbuf[0], s.cout, nullptr, 0, S, S};
                 break;
             }
@@ -382,29 +441,37 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 // the current activation must live in its own skip buffer
                 float* dst = hsbuf[hs_i];
                 if (cur.a != dst) {
-                    CFD_HIP(hipMemcpyAsync(dst, cur.a, sizeof(float) * (size_t)B * cur.H * cur.W * cur.Ca,
-                                           hipMemcpyDeviceToDevice, st));
+                    if (launch)
+                        CFD_HIP(hipMemcpyAsync(dst, cur.a, sizeof(float) * (size_t)B * cur.H * cur.W * cur.Ca,
+                                               hipMemcpyDeviceToDevice, st));
                     cur.a = dst;
                 }
-                stack.push_back(cur);
+                rec.push_hs = (int)hs_i;
+                stack.push_back({cur, (int)hs_i});
                 ++hs_i;
                 break;
             }
             case cfd::Step::Cat: {
-                const Act skip = stack.back();
+                const auto skip = stack.back();
                 stack.pop_back();
-                CFD_REQUIRE(cur.b == nullptr && skip.H == cur.H, CFD_ESTATE, "internal: concat shape");
-                cur.b = skip.a;
-                cur.Cb = skip.Ca;
+                CFD_REQUIRE(cur.b == nullptr && skip.first.H == cur.H, CFD_ESTATE, "internal: concat shape");
+                cur.b = skip.first.a;
+                cur.Cb = skip.first.Ca;
+                pending_skip = skip.second;
                 break;
             }
             case cfd::Step::Res: {
                 const auto& r = h->res[s.idx];
                 CFD_REQUIRE(cur.C() == r.cin, CFD_ESTATE, "internal: ResBlock input channels at " + r.pre);
+                rec.skip_hs = pending_skip;
+                pending_skip = -1;
+                const size_t nout = (size_t)B * cur.H * cur.W * r.cout;
                 // h = in_layers(x) + emb_layers(emb)   (unet.py:236-254)
-                const Act xin = gn(cur, r.pre + ".in_layers.0", 1);
-                conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, tmp);
-                const Act th{tmp, r.cout, nullptr, 0, cur.H, cur.W};
+                const Act xin = gn(cur, r.pre + ".in_layers.0", 1, &rec.ss1, &rec.st1);
+                float* hb = tape ? keep(nout) : tmp;
+                conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, hb);
+                rec.h1 = hb;
+                const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
                 // skip(x) + out_layers(h)   (unet.py:255-256)
                 const float* resp;
                 if (r.cin != r.cout) {
@@ -414,38 +481,46 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     CFD_REQUIRE(cur.b == nullptr, CFD_ESTATE, "identity skip on a concatenated input");
                     resp = cur.a;
                 }
-                const Act hn = gn(th, r.pre + ".out_layers.0", 1);
-                float* out = dest(cur.a, cur.b);
+                const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2);
+                float* out = dest(cur.a, cur.b, nout);
                 conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};
                 break;
             }
             case cfd::Step::Attn: {
                 const auto& at = h->attn[s.idx];
-                const Act xn = gn(cur, at.pre + ".norm", 0);
-                conv(xn, at.pre + ".qkv", 3 * at.C, 1, 1, 0, nullptr, nullptr, qkv);
-                cfd::AttnArgs aa{qkv, abuf, cur.H * cur.W, at.C, (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
-                cfd::launch_attention(aa, at.ch, at.heads, B, st);
-                float* out = dest(cur.a, nullptr);
-                conv(Act{abuf, at.C, nullptr, 0, cur.H, cur.W}, at.pre + ".proj_out", at.C, 1, 1, 0, nullptr, cur.a,
+                const int T = cur.H * cur.W;
+                const Act xn = gn(cur, at.pre + ".norm", 0, &rec.ss1, &rec.st1);
+                float* qb = tape ? keep((size_t)B * T * 3 * at.C) : qkv;
+                float* ob = tape ? keep((size_t)B * T * at.C) : abuf;
+                conv(xn, at.pre + ".qkv", 3 * at.C, 1, 1, 0, nullptr, nullptr, qb);
+                cfd::AttnArgs aa{qb, ob, T, at.C, (float)(1.0 / std::sqrt(std::sqrt((double)at.ch))), nullptr};
+                if (tape) aa.lse = keep((size_t)B * at.heads * T);
+                rec.qkv = qb;
+                rec.o = ob;
+                rec.lse = aa.lse;
+                if (launch) cfd::launch_attention(aa, at.ch, at.heads, B, st);
+                float* out = dest(cur.a, nullptr, (size_t)B * T * at.C);
+                conv(Act{ob, at.C, nullptr, 0, cur.H, cur.W}, at.pre + ".proj_out", at.C, 1, 1, 0, nullptr, cur.a,
                      out);
                 cur = Act{out, at.C, nullptr, 0, cur.H, cur.W};
                 break;
             }
             case cfd::Step::Down: {
-                float* out = dest(cur.a, nullptr);
+                const int Ho = (cur.H + 1) / 2, Wo = (cur.W + 1) / 2;
+                float* out = dest(cur.a, nullptr, (size_t)B * Ho * Wo * s.cout);
                 conv(cur, s.conv, s.cout, 3, 2, 0, nullptr, nullptr, out);
-                cur = Act{out, s.cout, nullptr, 0, (cur.H + 1) / 2, (cur.W + 1) / 2};
+                cur = Act{out, s.cout, nullptr, 0, Ho, Wo};
                 break;
             }
             case cfd::Step::Up: {
-                float* out = pick(cur.a, nullptr);
+                float* out = tape ? keep((size_t)B * 4 * cur.H * cur.W * s.cout) : pick(cur.a, nullptr);
                 conv(cur, s.conv, s.cout, 3, 1, 1, nullptr, nullptr, out);
                 cur = Act{out, s.cout, nullptr, 0, cur.H * 2, cur.W * 2};
                 break;
             }
             case cfd::Step::Out: {
-                const Act on = gn(cur, "out.0", 1);
+                const Act on = gn(cur, "out.0", 1, &rec.ss1, &rec.st1);
                 cfd::ConvArgs a{};
                 a.src1 = on.a;
                 a.C1 = on.Ca;
@@ -458,6 +533,185 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 a.Cout = c.out_channels;
                 a.M = B * cur.H * cur.W;
                 a.K = 9 * cur.Ca;
+                if (launch) cfd::launch_conv_out(a, st);
+                break;
+            }
+        }
+        if (recs) (*recs)[si] = rec;
+    }
+}
+
+
+// Input-gradient d_x = (d eps / d x)^T d_eps of the forward recorded in the tape
+// (DPS adjoint: the autograd.grad of grad_and_value through the U-Net,
+// condition_methods.py:31-47; weights are constants, so only data gradients).
+// Walks the steps in reverse; convolution input-gradients run on conv_gemm with
+// the transposed weight packs (stride-1/2 via TMODE, Upsample+conv as one 4x4
+// stride-2 convolution), GroupNorm(+SiLU) and attention backward in unet_vjp.hip.
+void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std::vector<Rec>& recs, Workspace& ws,
+             hipStream_t st) {
+    const auto& c = h->cfg;
+    const int S = c.image_size;
+    const Sizes z = sizes(h);
+    const size_t kSplitCap = split_cap(B);
+    float* splitk = ws.take(kSplitCap);
+    double* gnpart = (double*)ws.take((size_t)B * 64 * 32 * 2 * 2);
+    float* gnfin = ws.take((size_t)B * 64);
+    float* gpool[4];
+    for (auto& p : gpool) p = ws.take((size_t)B * z.max_cat);
+    float* dqkv = ws.take((size_t)B * z.max_qkv);
+    float* dd = ws.take((size_t)B * z.max_att);
+    std::vector<float*> dhs;
+    for (size_t n : z.hs) dhs.push_back(ws.take((size_t)B * n));
+    if (ws.dry) return;
+
+    auto gfree = [&](const float* b1, const float* b2 = nullptr, const float* b3 = nullptr) -> float* {
+        for (auto p : gpool)
+            if (p != b1 && p != b2 && p != b3) return p;
+        throw cfd::Error{CFD_ESTATE, "internal: gradient pool exhausted"};
+    };
+    // input-gradient of a convolution: dY (Hin x Win, Cin_bwd channels) -> dX (Hout x Wout, cout)
+    auto dconv = [&](const float* dy, int cin, int Hin, int Win, const std::string& key, int cout, int Hout, int Wout,
+                     int ks, int stride, int pad, int tmode, float* out) {
+        cfd::ConvArgs a{};
+        a.src1 = dy;
+        a.C1 = cin;
+        a.Ctot = cin;
+        a.w = PT(h, key);
+        a.out = out;
+        a.part = splitk;
+        a.Hin = Hin;
+        a.Win = Win;
+        a.Hout = Hout;
+        a.Wout = Wout;
+        a.stride = stride;
+        a.ks = ks;
+        a.pad = pad;
+        a.tmode = tmode;
+        a.Cout = cout;
+        a.M = B * Hout * Wout;
+        a.K = ks * ks * cin;
+        cfd::launch_conv(a, plan_checked(a, kSplitCap), st);
+    };
+    auto gnb = [&](const Act& in, const float* ss, const float* stats, const std::string& pre, int silu,
+                   const float* dz, const float* addsrc, float* out1, float* out2) {
+        cfd::GnbArgs g{};
+        g.x1 = in.a;
+        g.x2 = in.b;
+        g.dz = dz;
+        g.ss = ss;
+        g.stats = stats;
+        g.gamma = P(h, pre + ".weight");
+        g.addsrc = addsrc;
+        g.out1 = out1;
+        g.out2 = out2;
+        g.part = gnpart;
+        g.fin = gnfin;
+        g.C1 = in.Ca;
+        g.C2 = in.Cb;
+        g.Ctot = in.C();
+        g.HW = in.H * in.W;
+        g.silu = silu;
+        cfd::launch_gn_bwd(g, B, st);
+    };
+
+    Act dcur;  // gradient w.r.t. the current activation (single contiguous tensor)
+    for (size_t si = h->steps.size(); si-- > 0;) {
+        const auto& s = h->steps[si];
+        const Rec& r = recs[si];
+        const Act& in = r.in;
+        switch (s.kind) {
+            case cfd::Step::Out: {
+                // out.2 input-gradient (Cout <= 4 -> C): VALU gather with mirrored taps
+                float* G = gpool[0];
+                cfd::ConvArgs a{};
+                a.src1 = d_eps;
+                a.C1 = c.out_channels;
+                a.Ctot = c.out_channels;
+                a.w = PT(h, "out.2.weight");
+                a.out = G;
+                a.Hin = a.Hout = in.H;
+                a.Win = a.Wout = in.W;
+                a.Cout = in.Ca;
+                a.M = B * in.H * in.W;
+                a.tmode = 1;
+                cfd::launch_conv_in(a, st);
+                float* dh = gpool[1];
+                gnb(in, r.ss1, r.st1, "out.0", 1, G, nullptr, dh, nullptr);
+                dcur = Act{dh, in.Ca, nullptr, 0, in.H, in.W};
+                break;
+            }
+            case cfd::Step::Up: {
+                // nearest-2x + conv3x3 == one 4x4 stride-2 pad-1 convolution of dY (packed at set_param)
+                float* out = gfree(dcur.a);
+                dconv(dcur.a, dcur.Ca, dcur.H, dcur.W, s.conv + ".weight", s.cin, in.H, in.W, 4, 2, 1, 0, out);
+                dcur = Act{out, s.cin, nullptr, 0, in.H, in.W};
+                break;
+            }
+            case cfd::Step::Down: {
+                float* out = gfree(dcur.a);
+                dconv(dcur.a, dcur.Ca, dcur.H, dcur.W, s.conv + ".weight", s.cin, in.H, in.W, 3, 2, 1, 1, out);
+                dcur = Act{out, s.cin, nullptr, 0, in.H, in.W};
+                break;
+            }
+            case cfd::Step::Push:
+                // the pushed tensor's gradient also arrives through its skip concat
+                cfd::launch_add(const_cast<float*>(dcur.a), dhs[r.push_hs], (int64_t)B * dcur.H * dcur.W * dcur.Ca,
+                                st);
+                break;
+            case cfd::Step::Cat:
+                break;  // the concat's gradient split happens in the ResBlock that consumed it
+            case cfd::Step::Res: {
+                const auto& rs = h->res[s.idx];
+                const float* dout = dcur.a;
+                float* G = gfree(dout);
+                dconv(dout, rs.cout, in.H, in.W, rs.pre + ".out_layers.3.weight", rs.cout, in.H, in.W, 3, 1, 1, 1, G);
+                float* dh1 = gfree(dout, G);
+                gnb(Act{r.h1, rs.cout, nullptr, 0, in.H, in.W}, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr,
+                    dh1, nullptr);
+                // G <- in_layers conv input-gradient (Ctot channels)
+                dconv(dh1, rs.cout, in.H, in.W, rs.pre + ".in_layers.2.weight", in.C(), in.H, in.W, 3, 1, 1, 1, G);
+                const float* addsrc = dout;
+                if (rs.cin != rs.cout) {
+                    float* sk = gfree(dout, G, dh1);
+                    dconv(dout, rs.cout, in.H, in.W, rs.pre + ".skip_connection.weight", in.C(), in.H, in.W, 1, 1, 0,
+                          0, sk);
+                    addsrc = sk;
+                }
+                float* dx = dh1;  // dh1 is consumed: reuse for the first source's gradient
+                gnb(in, r.ss1, r.st1, rs.pre + ".in_layers.0", 1, G, addsrc, dx,
+                    in.b ? dhs[r.skip_hs] : nullptr);
+                dcur = Act{dx, in.Ca, nullptr, 0, in.H, in.W};
+                break;
+            }
+            case cfd::Step::Attn: {
+                const auto& at = h->attn[s.idx];
+                const int T = in.H * in.W;
+                const float* dout = dcur.a;
+                float* dA = gfree(dout);
+                dconv(dout, at.C, in.H, in.W, at.pre + ".proj_out.weight", at.C, in.H, in.W, 1, 1, 0, 0, dA);
+                cfd::AttnBwdArgs ab{r.qkv, r.o, dA, r.lse, dd, dqkv, T, at.C,
+                                    (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
+                cfd::launch_attention_bwd(ab, at.ch, at.heads, B, st);
+                float* dxn = gfree(dout, dA);
+                dconv(dqkv, 3 * at.C, in.H, in.W, at.pre + ".qkv.weight", at.C, in.H, in.W, 1, 1, 0, 0, dxn);
+                gnb(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn, dout, dA, nullptr);
+                dcur = Act{dA, at.C, nullptr, 0, in.H, in.W};
+                break;
+            }
+            case cfd::Step::In: {
+                cfd::ConvArgs a{};
+                a.src1 = dcur.a;
+                a.C1 = dcur.Ca;
+                a.Ctot = dcur.Ca;
+                a.w = PT(h, s.conv + ".weight");
+                a.out = d_x;
+                a.Hin = a.Hout = S;
+                a.Win = a.Wout = S;
+                a.Cout = c.in_channels;
+                a.M = B * S * S;
+                a.K = 9 * dcur.Ca;
+                a.tmode = 1;
                 cfd::launch_conv_out(a, st);
                 break;
             }
@@ -489,6 +743,7 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             CFD_HIP(hipMalloc(&h->arena, sizeof(float) * h->arena_floats));
             CFD_HIP(hipMalloc(&h->emb_w, sizeof(float) * (size_t)h->emb_total * h->tdim));
             CFD_HIP(hipMalloc(&h->emb_b, sizeof(float) * (size_t)h->emb_total));
+            CFD_HIP(hipMalloc(&h->arena_t, sizeof(float) * std::max<size_t>(h->arena_t_floats, 4)));
             const int half = cfg->model_channels / 2;
             // freqs = exp(-ln(10000) * arange(half, fp32) / half) in fp32 (nn.py:129-131)
             std::vector<float> fr(half);
@@ -510,6 +765,7 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->emb_w);
     (void)hipFree(h->emb_b);
     (void)hipFree(h->freqs);
+    (void)hipFree(h->arena_t);
     delete h;
 }
 
@@ -561,6 +817,35 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
                 CFD_HIP(hipMemcpy(h->emb_b + p.emb_row, host, n * 4, hipMemcpyHostToDevice));
                 break;
         }
+        if (p.tpack) {
+            // input-gradient packs.  1: W^T as (Cin, tap, Cout) (taps not mirrored:
+            // conv_gemm's TMODE gathers dY[(o + pad - tap) / stride]).  2: Upsample +
+            // conv3x3 as a 4x4 stride-2 pad-1 convolution of dY: per axis, tap e of
+            // the 4 sums the 3x3 taps d with a - d + 2 == e over the two nearest
+            // neighbours a in {0, 1}:  e0 = w2, e1 = w1 + w2, e2 = w0 + w1, e3 = w0.
+            const int64_t co = p.shape[0], ci = p.shape[1];
+            const int taps = (int)(p.count / (size_t)(co * ci));
+            std::vector<float> pk(p.tpack == 2 ? (size_t)ci * 16 * co : n);
+            if (p.tpack == 1) {
+                for (int64_t o = 0; o < co; ++o)
+                    for (int64_t i = 0; i < ci; ++i)
+                        for (int tap = 0; tap < taps; ++tap)
+                            pk[((size_t)i * taps + tap) * co + o] = host[((size_t)o * ci + i) * taps + tap];
+            } else {
+                static const int dlo[4] = {2, 1, 0, 0}, dhi[4] = {2, 2, 1, 0};
+                for (int64_t o = 0; o < co; ++o)
+                    for (int64_t i = 0; i < ci; ++i)
+                        for (int ey = 0; ey < 4; ++ey)
+                            for (int ex = 0; ex < 4; ++ex) {
+                                float v = 0.f;
+                                for (int dy = dlo[ey]; dy <= dhi[ey]; ++dy)
+                                    for (int dx = dlo[ex]; dx <= dhi[ex]; ++dx)
+                                        v += host[((size_t)o * ci + i) * 9 + dy * 3 + dx];
+                                pk[((size_t)i * 16 + ey * 4 + ex) * co + o] = v;
+                            }
+            }
+            CFD_HIP(hipMemcpy(h->arena_t + p.toffset, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
+        }
         p.set = true;
     });
 }
@@ -600,5 +885,72 @@ extern "C" int cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, f
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
         Workspace ws{(char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255)), 0, false};
         run(h, x, t, eps, B, ws, (hipStream_t)stream);
+    });
+}
+
+extern "C" int cfd_unet_tape_bytes(const cfd_unet* h, int B, size_t* bytes) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && bytes && B > 0, CFD_EARG, "bad argument");
+        Workspace ws{nullptr, 0, true}, tws{nullptr, 0, true};
+        Tape tape{&tws, nullptr};
+        run(h, nullptr, nullptr, nullptr, B, ws, nullptr, &tape, false);
+        *bytes = tws.off + 256;
+    });
+}
+
+extern "C" int cfd_unet_vjp_workspace_bytes(const cfd_unet* h, int B, size_t* bytes) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && bytes && B > 0, CFD_EARG, "bad argument");
+        Workspace ws{nullptr, 0, true};
+        std::vector<Rec> none;
+        run_vjp(h, nullptr, nullptr, B, none, ws, nullptr);
+        *bytes = ws.off + 256;
+    });
+}
+
+namespace {
+char* align256(void* p) { return (char*)(((uintptr_t)p + 255) & ~uintptr_t(255)); }
+
+void check_ready(const cfd_unet* h) {
+    for (const auto& p : h->params) CFD_REQUIRE(p.set, CFD_ESTATE, "U-Net parameter not set: " + p.key);
+}
+}  // namespace
+
+extern "C" int cfd_unet_forward_tape(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
+                                     void* workspace, size_t ws_bytes, void* tape, size_t tape_bytes, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && x && t && eps && workspace && tape, CFD_EARG, "null argument");
+        CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
+        check_ready(h);
+        size_t need = 0, tneed = 0;
+        cfd_unet_workspace_bytes(h, B, &need);
+        cfd_unet_tape_bytes(h, B, &tneed);
+        CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
+        CFD_REQUIRE(tape_bytes >= tneed, CFD_EARG, "tape too small");
+        Workspace ws{align256(workspace), 0, false}, tws{align256(tape), 0, false};
+        Tape tp{&tws, nullptr};
+        run(h, x, t, eps, B, ws, (hipStream_t)stream, &tp, true);
+    });
+}
+
+extern "C" int cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, int B, const void* tape,
+                                  size_t tape_bytes, void* workspace, size_t ws_bytes, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && d_eps && d_x && tape && workspace, CFD_EARG, "null argument");
+        CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
+        check_ready(h);
+        size_t need = 0, tneed = 0;
+        cfd_unet_vjp_workspace_bytes(h, B, &need);
+        cfd_unet_tape_bytes(h, B, &tneed);
+        CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
+        CFD_REQUIRE(tape_bytes >= tneed, CFD_EARG, "tape too small");
+        // replay the forward walk (no launches) over the same tape layout to
+        // recover where every saved activation lives
+        Workspace fws{nullptr, 0, true}, tws{align256(const_cast<void*>(tape)), 0, false};
+        std::vector<Rec> recs;
+        Tape tp{&tws, &recs};
+        run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
+        Workspace ws{align256(workspace), 0, false};
+        run_vjp(h, d_eps, d_x, B, recs, ws, (hipStream_t)stream);
     });
 }

@@ -94,6 +94,10 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnArgs a) {
         const double var = fmax(s2 / n - mean * mean, 0.0);
         sh_mean[grp] = (float)mean;
         sh_rstd[grp] = (float)(1.0 / sqrt(var + (double)a.eps));
+        if (a.stats) {
+            a.stats[(b * 32 + grp) * 2 + 0] = sh_mean[grp];
+            a.stats[(b * 32 + grp) * 2 + 1] = sh_rstd[grp];
+        }
     }
     __syncthreads();
     for (int c = threadIdx.x; c < Ctot; c += blockDim.x) {
@@ -139,10 +143,13 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
 // (no integer division in the K loop).  Register-staged double buffer.
 // Optional split-K (gridDim.z > 1): partial sums go to a (split, M, N) slab and
 // splitk_reduce applies the epilogue.
+// TMODE: transposed addressing for the input-gradient of a stride-s convolution
+// (DPS adjoint): output pixel o gathers dY[(o + pad - tap) / s] where divisible,
+// with weights packed (Cin_fwd, tap, Cout_fwd).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 32 + 4 * (chunk ^ ((row ^ (row >> 1)) & 7)); }
 
-template <int BM, int BN>
+template <int BM, int BN, bool TMODE>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     constexpr int BK = 32;
     constexpr int WM = BM / 2, WN = BN / 2;
@@ -168,7 +175,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         const int rem = mm - a_b[it] * HWo;
         a_oy[it] = rem / a.Wout;
         a_ox[it] = rem - a_oy[it] * a.Wout;
-        if (!a.up) {
+        if (TMODE) {
+            a_oy[it] += a.pad;
+            a_ox[it] += a.pad;
+        } else if (!a.up) {
             a_oy[it] = a_oy[it] * a.stride - a.pad;
             a_ox[it] = a_ox[it] * a.stride - a.pad;
         } else {
@@ -198,19 +208,31 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         dx = tap - dy * a.ks;
     }
 
+    const int smask = a.stride - 1, sshift = a.stride >> 1;
     f4 ra[AIT], rb[BIT];
     auto load_tile = [&](int kt) {
         const int c0 = cb + 4 * kq;
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             f4 v = {0.f, 0.f, 0.f, 0.f};
-            int iy = a_oy[it] + dy, ix = a_ox[it] + dx;
+            int iy, ix;
             bool ok = a_ok[it];
-            if (a.up) {
+            if (TMODE) {
+                iy = a_oy[it] - dy;
+                ix = a_ox[it] - dx;
+                ok = ok && iy >= 0 && ix >= 0 && ((iy | ix) & smask) == 0;
+                iy >>= sshift;
+                ix >>= sshift;
+                ok = ok && iy < a.Hin && ix < a.Win;
+            } else if (a.up) {
+                iy = a_oy[it] + dy;
+                ix = a_ox[it] + dx;
                 ok = ok && iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
                 iy >>= 1;
                 ix >>= 1;
             } else {
+                iy = a_oy[it] + dy;
+                ix = a_ox[it] + dx;
                 ok = ok && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
             }
             if (ok) {
@@ -302,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
             for (int j = 0; j < TN; ++j) {
                 const int n = n0 + wn * WN + 16 * j + li;
                 if (n >= a.Cout) continue;
-                float v = acc[i][j][r] + a.bias[n];
+                float v = a.bias ? acc[i][j][r] + a.bias[n] : acc[i][j][r];
                 if (a.emb) v = v + a.emb[(int64_t)bb * a.emb_stride + n];
                 if (a.res) v = a.res[(int64_t)m * a.Cout + n] + v;
                 a.out[(int64_t)m * a.Cout + n] = v;
@@ -325,7 +347,7 @@ __global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
     f4 v;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        float y = s[j] + a.bias[n + j];
+        float y = a.bias ? s[j] + a.bias[n + j] : s[j];
         if (a.emb) y = y + a.emb[(int64_t)bb * a.emb_stride + n + j];
         if (a.res) y = a.res[i + j] + y;
         v[j] = y;
@@ -334,6 +356,8 @@ __global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
 }
 
 // First convolution, in_channels (<= 4) -> Cout, 3x3 pad 1: VALU, one output per thread.
+// tmode: the same gather with the taps mirrored (input-gradient of the last
+// convolution, weights packed (Cin_fwd, tap, Cout_fwd)); bias may be null.
 __global__ void conv_in_kernel(ConvArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)a.M * a.Cout) return;
@@ -343,12 +367,13 @@ __global__ void conv_in_kernel(ConvArgs a) {
     const int b = m / HW, rem = m - b * HW, oy = rem / a.Wout, ox = rem - oy * a.Wout;
     float s = 0.f;
     for (int tap = 0; tap < 9; ++tap) {
-        const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+        const int ty = a.tmode ? 1 - tap / 3 : tap / 3 - 1, tx = a.tmode ? 1 - tap % 3 : tap % 3 - 1;
+        const int iy = oy + ty, ix = ox + tx;
         if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
         const float* px = a.src1 + (((int64_t)b * a.Hin + iy) * a.Win + ix) * a.C1;
         for (int c = 0; c < a.C1; ++c) s = fmaf(a.w[((int64_t)n * 9 + tap) * a.C1 + c], px[c], s);
     }
-    a.out[idx] = s + a.bias[n];
+    a.out[idx] = a.bias ? s + a.bias[n] : s;
 }
 
 // Last convolution (input already GroupNorm+SiLU'd), Ctot -> Cout (<= 4), 3x3 pad 1.  One wave
@@ -362,7 +387,8 @@ __global__ void conv_out_kernel(ConvArgs a) {
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     for (int k = lane; k < a.K; k += 64) {
         const int tap = k / a.Ctot, c = k - tap * a.Ctot;
-        const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+        const int ty = a.tmode ? 1 - tap / 3 : tap / 3 - 1, tx = a.tmode ? 1 - tap % 3 : tap % 3 - 1;
+        const int iy = oy + ty, ix = ox + tx;
         if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
         const float v = a.src1[(((int64_t)b * a.Hin + iy) * a.Win + ix) * a.C1 + c];
         for (int n = 0; n < a.Cout; ++n) s[n] = fmaf(a.w[(int64_t)n * a.K + k], v, s[n]);
@@ -370,7 +396,7 @@ __global__ void conv_out_kernel(ConvArgs a) {
     for (int n = 0; n < a.Cout; ++n) {
         float v = s[n];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0) a.out[m * a.Cout + n] = v + a.bias[n];
+        if (lane == 0) a.out[m * a.Cout + n] = a.bias ? v + a.bias[n] : v;
     }
 }
 
@@ -462,6 +488,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
     }
     // lane (g, li) holds O[query li][16 d + 4 g + r]
     const int tq = q0 + li;
+    if (a.lse && g == 0 && tq < T) a.lse[((int64_t)b * gridDim.y + h) * T + tq] = mrun + logf(lrun);
     if (tq < T) {
         float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
         const float inv = 1.0f / lrun;
@@ -552,23 +579,34 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     const int nkt = a.K / 32;
     p.splits = 1;
     while (tiles(p.bm) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16) p.splits *= 2;
-    while (p.splits > 1 && (size_t)p.splits * a.M * a.Cout > part_cap_floats) p.splits /= 2;  // memory guard
+    // memory guard, on the nominal shape too: part_cap_floats is the slab per 8
+    // samples (the caller sizes the real slab as ceil(B/8) of these)
+    while (p.splits > 1 && (size_t)p.splits * mn * a.Cout > part_cap_floats) p.splits /= 2;
     return p;
+}
+
+template <bool TMODE>
+static void launch_conv_tiles(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
+    if (p.bm == 128 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE>), grid, dim3(256), 0, st, a);
+    else if (p.bm == 64 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE>), grid, dim3(256), 0, st, a);
+    else if (p.bm == 128 && p.bn == 64)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 64, TMODE>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE>), grid, dim3(256), 0, st, a);
 }
 
 void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
     CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot, CFD_ESHAPE, "conv K mismatch");
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
+    CFD_REQUIRE(!a.tmode || ((a.stride == 1 || a.stride == 2) && !a.up), CFD_ESHAPE, "transposed conv: stride 1|2");
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
-    if (p.bm == 128 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 128>), grid, dim3(256), 0, st, a);
-    else if (p.bm == 64 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 128>), grid, dim3(256), 0, st, a);
-    else if (p.bm == 128 && p.bn == 64)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 64>), grid, dim3(256), 0, st, a);
+    if (a.tmode)
+        launch_conv_tiles<true>(a, p, grid, st);
     else
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 64>), grid, dim3(256), 0, st, a);
+        launch_conv_tiles<false>(a, p, grid, st);
     check_launch("conv_gemm_kernel");
     if (p.splits > 1) {
         const int64_t total4 = (int64_t)a.M * a.Cout / 4;

@@ -12,6 +12,7 @@ struct GnArgs {
     double* part;       // (B, nchunks, 32, 2) partial sums
     float* ss;          // (B, Ctot, 2) scale / shift
     float* out;         // (B, HW, Ctot) normalised (+ SiLU) activation
+    float* stats;       // optional (B, 32, 2) group mean / rstd (kept for the backward)
     int C1, C2, Ctot, HW;
     float eps;
     int silu;
@@ -23,7 +24,7 @@ struct ConvArgs {
     const float* src1;
     const float* src2;   // concat-free second source (channels C1..C1+C2) or null
     const float* w;      // packed (Cout, ks*ks, Ctot)
-    const float* bias;   // (Cout)
+    const float* bias;   // (Cout) or null
     const float* emb;    // (B, emb_stride) slice, or null
     const float* res;    // (M, Cout) residual, or null
     float* out;          // (M, Cout)
@@ -31,6 +32,7 @@ struct ConvArgs {
     int C1, C2, Ctot;
     int Hin, Win, Hout, Wout;
     int stride, ks, pad, up;
+    int tmode;           // transposed addressing (input-gradient of a stride-s conv)
     int Cout;
     int emb_stride;
     int M, K;
@@ -41,6 +43,38 @@ struct AttnArgs {
     float* out;        // (B, T, C)
     int T, C;
     float scale;       // 1/sqrt(sqrt(ch)), applied to q and k separately
+    float* lse;        // optional (B, heads, T) log-sum-exp of each softmax row
+};
+
+// GroupNorm(32)(+SiLU) backward: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),
+// g = gamma * dz (* SiLU'(z)), per (sample, group).  dx is split over the two
+// forward sources: channels [0, C1) -> out1 (stride C1), [C1, Ctot) -> out2.
+struct GnbArgs {
+    const float* x1;
+    const float* x2;      // forward input sources
+    const float* dz;      // (B, HW, Ctot) gradient w.r.t. the GN(+SiLU) output
+    const float* ss;      // (B, Ctot, 2) forward scale / shift
+    const float* stats;   // (B, 32, 2) forward mean / rstd
+    const float* gamma;
+    const float* addsrc;  // optional (B, HW, Ctot) added to dx (residual branch)
+    float* out1;
+    float* out2;
+    int acc1, acc2;       // accumulate into out1 / out2 instead of overwriting
+    double* part;         // scratch (B, nchunks, 32, 2)
+    float* fin;           // scratch (B, 32, 2)
+    int C1, C2, Ctot, HW, silu, nchunks, B;
+};
+
+// QKVAttentionLegacy backward (flash-style, recomputes P from the saved LSE).
+struct AttnBwdArgs {
+    const float* qkv;   // (B, T, 3C) forward input
+    const float* o;     // (B, T, C) forward output (before proj_out)
+    const float* dout;  // (B, T, C) gradient w.r.t. o
+    const float* lse;   // (B, heads, T)
+    float* dd;          // scratch (B, heads, T): rowsum(dO * O)
+    float* dqkv;        // (B, T, 3C)
+    int T, C;
+    float scale;
 };
 
 struct ConvPlan {
@@ -50,11 +84,17 @@ struct ConvPlan {
 int gn_chunks(int HW);
 // GroupNorm statistics + normalise (+SiLU) into a.out
 void launch_gn(const GnArgs& a, int B, hipStream_t st);
+// part_cap_floats: split-K slab available per 8 samples (plans depend on the
+// per-sample shape only, never on the batch)
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats);
 void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st);
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
 void launch_conv_out(const ConvArgs& a, hipStream_t st);
 void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t st);
+// backward (unet_vjp.hip)
+void launch_gn_bwd(const GnbArgs& a, int B, hipStream_t st);
+void launch_attention_bwd(const AttnBwdArgs& a, int CH, int heads, int B, hipStream_t st);
+void launch_add(float* y, const float* x, int64_t n, hipStream_t st);
 void launch_temb(const int64_t* t, const float* freqs, float* out, int dim, int B, hipStream_t st);
 void launch_linear(const float* x, const float* W, const float* bias, float* y, int B, int K, int N, int act,
                    hipStream_t st);

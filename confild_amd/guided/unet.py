@@ -1,0 +1,43 @@
+"""create_model of the conditional notebook (C/src/guided_diffusion/unet.py:25-92)."""
+from __future__ import annotations
+
+import torch
+
+from ..unet import UNetModel
+
+NUM_CLASSES = 1000
+
+
+def create_model(image_size, num_channels, num_res_blocks, out_channels=1, channel_mult="", learn_sigma=False,
+                 class_cond=False, use_checkpoint=False, attention_resolutions="16", num_heads=1, num_head_channels=-1,
+                 num_heads_upsample=-1, use_scale_shift_norm=False, dropout=0, resblock_updown=False, use_fp16=False,
+                 use_new_attention_order=False, model_path=""):
+    """Same arguments and the same checkpoint behaviour as the reference: a
+    load failure prints the exception and keeps the random initialisation
+    (C/unet.py:86-90).  Checkpoints load with weights_only=True."""
+    if channel_mult == "":
+        table = {512: (0.5, 1, 1, 2, 2, 4, 4), 256: (1, 1, 2, 2, 4, 4), 128: (1, 1, 2, 3, 4), 64: (1, 2, 3, 4)}
+        if image_size not in table:
+            raise ValueError(f"unsupported image size: {image_size}")
+        channel_mult = table[image_size]
+    else:
+        channel_mult = tuple(int(ch_mult) for ch_mult in channel_mult.split(","))
+    if isinstance(attention_resolutions, int):
+        attention_ds = [image_size // attention_resolutions]
+    elif isinstance(attention_resolutions, str):
+        attention_ds = [image_size // int(res) for res in attention_resolutions.split(",")]
+    else:
+        raise NotImplementedError
+    model = UNetModel(image_size=image_size, in_channels=out_channels, model_channels=num_channels,
+                      out_channels=(out_channels if not learn_sigma else 2 * out_channels),
+                      num_res_blocks=num_res_blocks, attention_resolutions=tuple(attention_ds), dropout=dropout,
+                      channel_mult=channel_mult, num_classes=(NUM_CLASSES if class_cond else None),
+                      use_checkpoint=use_checkpoint, use_fp16=use_fp16, num_heads=num_heads,
+                      num_head_channels=num_head_channels, num_heads_upsample=num_heads_upsample,
+                      use_scale_shift_norm=use_scale_shift_norm, resblock_updown=resblock_updown,
+                      use_new_attention_order=use_new_attention_order)
+    try:
+        model.load_state_dict(torch.load(model_path, map_location="cpu", weights_only=True))
+    except Exception as e:  # the reference's behaviour (unet.py:86-90)
+        print(f"Got exception: {e} / Randomly initialize")
+    return model

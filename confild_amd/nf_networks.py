@@ -112,19 +112,9 @@ class SIRENAutodecoder_film(nn.Module):
         b = latents.shape[0] if latents.dim() >= 2 else 1
         return coords.reshape(-1, d), latents.reshape(b, L), spatial
 
-    def decode(self, coords, latents, x_normalizer=None, y_normalizer=None):
-        """denorm(NF(norm(coords), latents)) in one fused launch (trainer.infer,
-        N/scripts/train.py:265-279; pass_through_model_batch, inference_function.py:22-48)."""
-        d, L, c = self.in_coord_features, self.in_latent_features, self.out_features
-        dev = latents.device
-        if dev.type != "cuda":
-            raise _lib.CfdError("SIREN decode needs GPU tensors (the HIP path has no CPU fallback)")
-        if latents.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("gradients through the SIREN decoder (DPS) are not built yet")
-        cf, lat, spatial = self._flatten(coords, latents, d, L)
-        cf = cf.to(device=dev, dtype=torch.float32).contiguous()
-        lat = lat.detach().to(torch.float32).contiguous()
-        N = cf.shape[0]
+    def _norm_args(self, cf, N, dev, x_normalizer, y_normalizer):
+        """Fusable '-11' normaliser bounds -> (coords, xmax, xmin, ymax, ymin, ystride, post)."""
+        d, c = self.in_coord_features, self.out_features
         xmax = xmin = ymax = ymin = None
         ystride = 0
         if x_normalizer is not None:
@@ -150,6 +140,23 @@ class SIRENAutodecoder_film(nn.Module):
                     raise ValueError(f"output normaliser params of {ymax.numel()} values match neither (c) nor (N, c)")
                 ymax = ymax.reshape(-1).contiguous()
                 ymin = ymin.reshape(-1).contiguous()
+        return cf, xmax, xmin, ymax, ymin, ystride, post
+
+    def decode(self, coords, latents, x_normalizer=None, y_normalizer=None):
+        """denorm(NF(norm(coords), latents)) in one fused launch (trainer.infer,
+        N/scripts/train.py:265-279; pass_through_model_batch, inference_function.py:22-48)."""
+        d, L, c = self.in_coord_features, self.in_latent_features, self.out_features
+        dev = latents.device
+        if dev.type != "cuda":
+            raise _lib.CfdError("SIREN decode needs GPU tensors (the HIP path has no CPU fallback)")
+        if latents.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("torch autograd does not run through the HIP SIREN: use tape_forward + "
+                                      "tape_vjp (the DPS sampler in confild_amd.guided does)")
+        cf, lat, spatial = self._flatten(coords, latents, d, L)
+        cf = cf.to(device=dev, dtype=torch.float32).contiguous()
+        lat = lat.detach().to(torch.float32).contiguous()
+        N = cf.shape[0]
+        cf, xmax, xmin, ymax, ymin, ystride, post = self._norm_args(cf, N, dev, x_normalizer, y_normalizer)
         h = self._handle(dev)
         b = lat.shape[0]
         nbytes = C.c_size_t()
@@ -163,6 +170,51 @@ class SIRENAutodecoder_film(nn.Module):
         if post is not None:
             out = post.denormalize(out)
         return out.reshape((b,) + spatial + (c,))
+
+    # -- latent gradient at a few query points (DPS measurement operator) ---------
+    def tape_forward(self, coords, latents, x_normalizer=None, y_normalizer=None):
+        """decode() of R latent rows (R, L) at Ns points (Ns, d) -> (R, Ns, c), keeping the
+        per-layer pre-activations for tape_vjp.  Only '-11' normalisers (fused)."""
+        d, L, c = self.in_coord_features, self.in_latent_features, self.out_features
+        dev = latents.device
+        if dev.type != "cuda":
+            raise _lib.CfdError("SIREN tape_forward needs GPU tensors (the HIP path has no CPU fallback)")
+        cf = coords.reshape(-1, d).to(device=dev, dtype=torch.float32).contiguous()
+        lat = latents.detach().reshape(-1, L).to(torch.float32).contiguous()
+        Ns, R = cf.shape[0], lat.shape[0]
+        cf, xmax, xmin, ymax, ymin, ystride, post = self._norm_args(cf, Ns, dev, x_normalizer, y_normalizer)
+        if post is not None or (x_normalizer is not None and xmax is None):
+            raise NotImplementedError("the SIREN latent gradient fuses '-11' normalisers only")
+        h = self._handle(dev)
+        lib = _lib.load()
+        n = C.c_size_t()
+        _lib.check(lib.cfd_siren_vjp_workspace_bytes(h, Ns, R, C.byref(n)), "siren vjp workspace")
+        ws = torch.empty(max(n.value, 16), dtype=torch.uint8, device=dev)
+        out = torch.empty((R, Ns, c), dtype=torch.float32, device=dev)
+        _lib.check(lib.cfd_siren_tape_forward(h, _lib.ptr(cf), Ns, _lib.ptr(lat), R, _lib.ptr(xmax), _lib.ptr(xmin),
+                                              _lib.ptr(ymax), _lib.ptr(ymin), ystride, _lib.ptr(out), _lib.ptr(ws),
+                                              ws.numel(), _lib.stream_of(dev)), "cfd_siren_tape_forward")
+        # keep every buffer the kernels read until tape_vjp
+        self._vjp_tape = (ws, Ns, R, ymax, ymin, ystride, cf, lat, xmax, xmin, self._signature())
+        return out
+
+    def tape_vjp(self, g_out):
+        """d<g_out, tape_forward(...)>/d latents -> (R, L), for the last tape_forward."""
+        tape = getattr(self, "_vjp_tape", None)
+        if tape is None:
+            raise RuntimeError("tape_vjp needs a preceding tape_forward")
+        ws, Ns, R, ymax, ymin, ystride, _, _, _, _, sig = tape
+        if sig != self._signature():
+            raise RuntimeError("parameters changed since tape_forward")
+        if tuple(g_out.shape) != (R, Ns, self.out_features) or g_out.device != ws.device:
+            raise ValueError("g_out must match the output of the last tape_forward")
+        g = g_out.detach().to(torch.float32).contiguous()
+        gz = torch.empty((R, self.in_latent_features), dtype=torch.float32, device=ws.device)
+        h = self._handle(ws.device)
+        _lib.check(_lib.load().cfd_siren_tape_vjp(h, _lib.ptr(g), Ns, R, _lib.ptr(ymax), _lib.ptr(ymin), ystride,
+                                                  _lib.ptr(gz), _lib.ptr(ws), ws.numel(), _lib.stream_of(ws.device)),
+                   "cfd_siren_tape_vjp")
+        return gz
 
     def forward(self, coords, latents):
         """nf_networks.py:480-495 (raw, un-normalised in and out)."""

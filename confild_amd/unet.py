@@ -254,15 +254,11 @@ class UNetModel(nn.Module):
             self._workspaces = {key: ws}  # keep one workspace (largest recent B)
         return ws
 
-    def forward(self, x: torch.Tensor, timesteps: torch.Tensor, y=None) -> torch.Tensor:
-        """UNetModel.forward (unet.py:634-663): (B, C, H, W) fp32, (B,) timesteps -> eps."""
+    def _prep(self, x, timesteps, y=None):
         if y is not None:
             raise NotImplementedError("class-conditional U-Net is not part of the CoNFiLD path")
         if x.device.type != "cuda":
             raise _lib.CfdError("UNetModel.forward: input must be on the GPU (the HIP path has no CPU fallback)")
-        if x.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("input gradients through the U-Net (DPS adjoint, SURVEY 8f rank 1) "
-                                      "are not built yet")
         B, Cin, H, W = x.shape
         if Cin != self.in_channels or H != self.image_size or W != self.image_size:
             raise ValueError(f"expected (B, {self.in_channels}, {self.image_size}, {self.image_size}), got "
@@ -274,12 +270,71 @@ class UNetModel(nn.Module):
         t = timesteps.to(device=x.device, dtype=torch.int64).contiguous()
         if t.shape != (B,):
             raise ValueError("timesteps must have shape (B,)")
+        return x, t, B
+
+    def forward(self, x: torch.Tensor, timesteps: torch.Tensor, y=None) -> torch.Tensor:
+        """UNetModel.forward (unet.py:634-663): (B, C, H, W) fp32, (B,) timesteps -> eps."""
+        if x.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("torch autograd does not run through the HIP U-Net: use forward_tape + "
+                                      "input_vjp (the DPS sampler in confild_amd.guided does)")
+        x, t, B = self._prep(x, timesteps, y)
         h = self._handle(x.device)
         ws = self._workspace(h, x.device, B)
-        eps = torch.empty((B, self.out_channels, H, W), dtype=torch.float32, device=x.device)
+        eps = torch.empty((B, self.out_channels, self.image_size, self.image_size), dtype=torch.float32,
+                          device=x.device)
         _lib.check(_lib.load().cfd_unet_forward(h, _lib.ptr(x), _lib.ptr(t), _lib.ptr(eps), B, _lib.ptr(ws),
                                                 ws.numel(), _lib.stream_of(x.device)), "cfd_unet_forward")
         return eps
+
+    # -- input-gradient (DPS adjoint) ---------------------------------------------
+    def forward_tape(self, x: torch.Tensor, timesteps: torch.Tensor) -> torch.Tensor:
+        """forward() that also records the activations for input_vjp (bit-identical eps)."""
+        x, t, B = self._prep(x, timesteps)
+        h = self._handle(x.device)
+        lib = _lib.load()
+        ws = self._workspace(h, x.device, B)
+        tape = self._tape_buf(h, x.device, B)
+        eps = torch.empty((B, self.out_channels, self.image_size, self.image_size), dtype=torch.float32,
+                          device=x.device)
+        _lib.check(lib.cfd_unet_forward_tape(h, _lib.ptr(x), _lib.ptr(t), _lib.ptr(eps), B, _lib.ptr(ws), ws.numel(),
+                                             _lib.ptr(tape), tape.numel(), _lib.stream_of(x.device)),
+                   "cfd_unet_forward_tape")
+        self._taped = (x.device, B, self._signature())
+        return eps
+
+    def input_vjp(self, d_eps: torch.Tensor) -> torch.Tensor:
+        """(d eps / d x)^T d_eps for the inputs of the last forward_tape (weights are constants)."""
+        if getattr(self, "_taped", None) is None:
+            raise RuntimeError("input_vjp needs a preceding forward_tape")
+        dev, B, sig = self._taped
+        if sig != self._signature():
+            raise RuntimeError("parameters changed since forward_tape")
+        if tuple(d_eps.shape) != (B, self.out_channels, self.image_size, self.image_size) or d_eps.device != dev:
+            raise ValueError("d_eps must match the eps of the last forward_tape")
+        h = self._handle(dev)
+        lib = _lib.load()
+        d_eps = d_eps.detach().to(torch.float32).contiguous()
+        tape = self._tape_buf(h, dev, B)
+        key = ("vjp", dev, B)
+        ws = self._vjp_ws if getattr(self, "_vjp_key", None) == key else None
+        if ws is None:
+            n = C.c_size_t()
+            _lib.check(lib.cfd_unet_vjp_workspace_bytes(h, B, C.byref(n)), "vjp workspace")
+            ws = self._vjp_ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+            self._vjp_key = key
+        d_x = torch.empty((B, self.in_channels, self.image_size, self.image_size), dtype=torch.float32, device=dev)
+        _lib.check(lib.cfd_unet_input_vjp(h, _lib.ptr(d_eps), _lib.ptr(d_x), B, _lib.ptr(tape), tape.numel(),
+                                          _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)), "cfd_unet_input_vjp")
+        return d_x
+
+    def _tape_buf(self, h, device, B):
+        key = (device, B)
+        if getattr(self, "_tape_key", None) != key:
+            n = C.c_size_t()
+            _lib.check(_lib.load().cfd_unet_tape_bytes(h, B, C.byref(n)), "tape bytes")
+            self._tape = torch.empty(n.value, dtype=torch.uint8, device=device)
+            self._tape_key = key
+        return self._tape
 
     def __del__(self):
         try:

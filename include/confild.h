@@ -76,6 +76,20 @@ int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
 int  cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                       void* workspace, size_t ws_bytes, void* stream);
 
+/* Input-gradient of the U-Net (DPS adjoint; replaces the autograd.grad of
+ * grad_and_value through UNetModel.forward, C/src/guided_diffusion/
+ * condition_methods.py:31-47, C/unet.py).  cfd_unet_forward_tape is
+ * cfd_unet_forward (bit-identical eps) that also keeps every activation the
+ * backward needs in `tape`; cfd_unet_input_vjp then computes
+ * d_x = (d eps / d x)^T d_eps for that forward (same h, B and tape).  Weights are
+ * constants: no parameter gradients. */
+int  cfd_unet_tape_bytes(const cfd_unet* h, int B, size_t* bytes);
+int  cfd_unet_vjp_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
+int  cfd_unet_forward_tape(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
+                           void* workspace, size_t ws_bytes, void* tape, size_t tape_bytes, void* stream);
+int  cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, int B, const void* tape,
+                        size_t tape_bytes, void* workspace, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Diffusion step epilogue (replaces p_mean_variance + p_sample / ddim_sample */
 /* for EPSILON / FIXED_LARGE, U/src/gaussian_diffusion.py:232-326,395-439,    */
@@ -109,6 +123,21 @@ int  cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, uint64_t 
  * max/min broadcast over the trailing `period` elements (period=1: scalars). */
 int  cfd_latent_denorm(const float* x, float* y, int64_t n, const float* vmax, const float* vmin,
                        int64_t period, void* stream);
+
+/* DPS glue (Case4 conditional sampling, C/src/guided_diffusion/condition_methods.py:31-47,81-90):
+ *   cfd_dps_residual     per sample: norm_b = ||y - A_b||_2, g_A = -(y - A_b) / norm_b
+ *                        (y shared when y_batch_stride == 0, else per sample);
+ *   cfd_dps_latent_grad  g_z (d norm / d unnormalised latent) -> d_eps = -srm1 * g and
+ *                        g_direct = sra * g, g = clamp'(x0) * g_z * (max - min) / 2
+ *                        (Case4Operator._unnorm, measurements.py:219-220);
+ *   cfd_dps_update       x_out = sample - (g_direct + g_unet) * scale. */
+int  cfd_dps_residual(const float* y, int64_t y_batch_stride, const float* A, float* g_A, float* norm,
+                      int64_t n_per_sample, int B, void* stream);
+int  cfd_dps_latent_grad(const cfd_sched* s, int clip, const float* x, const float* eps, const int64_t* t,
+                         const float* g_z, const float* vmax, const float* vmin, int64_t period,
+                         float* d_eps, float* g_direct, int64_t n_per_sample, int B, void* stream);
+int  cfd_dps_update(const float* sample, const float* g_direct, const float* g_unet, float scale,
+                    float* x_out, int64_t n, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Conditional neural field decoder: SIRENAutodecoder_film                    */
@@ -144,6 +173,22 @@ int  cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, const float
                        const float* xmax, const float* xmin,
                        const float* ymax, const float* ymin, int64_t y_stride,
                        float* out, void* workspace, size_t ws_bytes, void* stream);
+
+/* Latent-gradient of the Case4 measurement operator (DPS; replaces autograd
+ * through Case4Operator.forward -> pass_through_model_batch -> SIRENAutodecoder_film,
+ * C/src/guided_diffusion/measurements.py:219-226, N/cnf/inference_function.py:22-48).
+ * cfd_siren_tape_forward = cfd_siren_forward over Ns sensor coordinates for R
+ * latent rows, keeping each layer's pre-activation in the workspace;
+ * cfd_siren_tape_vjp: g_latents (R, L) = d<g_out, out>/d latents for that forward
+ * (same h, Ns, R, workspace and y normaliser). */
+int  cfd_siren_vjp_workspace_bytes(const cfd_siren* h, int64_t Ns, int R, size_t* bytes);
+int  cfd_siren_tape_forward(cfd_siren* h, const float* coords, int64_t Ns, const float* latents, int R,
+                            const float* xmax, const float* xmin,
+                            const float* ymax, const float* ymin, int64_t y_stride,
+                            float* out, void* workspace, size_t ws_bytes, void* stream);
+int  cfd_siren_tape_vjp(cfd_siren* h, const float* g_out, int64_t Ns, int R,
+                        const float* ymax, const float* ymin, int64_t y_stride,
+                        float* g_latents, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,7 @@ from confild_amd import synth
 from oracle import diffusion as od
 from oracle import siren as osn
 from oracle import unet as ou
+from oracle import dps as odps
 
 SCHED = golden("schedules.npz")
 RESP = {"id": "", "s256": "256", "ddim50": "ddim50", "ddim5": "ddim5", "s8": "8",
@@ -115,3 +116,41 @@ def test_synth_generator_is_stable():
     assert not np.array_equal(u, synth.uniform(1235, "input_blocks.0.0.weight", (4,), -1.0, 1.0))
     n = synth.normal(7, "x", (10001,))
     assert abs(float(n.mean())) < 0.05 and abs(float(n.std()) - 1) < 0.05
+
+
+# ---------------------------------------------------------------------------
+# DPS (Case4 conditional): the oracle's autograd DPS
+# loop replays the reference's own guided sampler run (make_golden_dps.py)
+# ---------------------------------------------------------------------------
+def dps_case(name):
+    """(golden, Tables, unet, operator, siren sd) of a DPS fixture, CPU oracle."""
+    from oracle import diffusion as od
+    g = golden(f"{name}.npz")
+    kw = ast.literal_eval(str(g["kwargs"]))
+    cfg = ou.Config(**kw)
+    sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(int(g["seed"]), ou.param_shapes(cfg)).items()}
+    d, L, c, nh, H = (int(v) for v in g["siren_dims"])
+    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(int(g["siren_seed"]), d, L, c, nh, H).items()}
+    tb = od.Tables(1000, "cosine", str(g["respacing"]))
+    T = lambda k: torch.from_numpy(g[k])  # noqa: E731
+    operator = lambda x0: odps.case4_forward(ssd, T("coords"), T("xhi"), T("xlo"), T("yhi"), T("ylo"),  # noqa: E731
+                                             T("vmax"), T("vmin"), x0, batch=int(g["op_batch"]))
+    unet = lambda x, t: ou.forward(sd, cfg, x, t)  # noqa: E731
+    return g, tb, unet, operator, ssd
+
+
+@pytest.mark.parametrize("name", ["dps_tiny16", "dps_tiny16_s3"])
+def test_dps_loop_matches_reference(name):
+    g, tb, unet, operator, _ = dps_case(name)
+    assert np.array_equal(tb.timestep_map, g["timestep_map"])
+    with torch.no_grad():
+        assert np.abs(operator(torch.from_numpy(g["x_true"])).numpy() - g["measurement"]).max() < 1e-6
+    _, traj = odps.dps_loop(tb, unet, operator, torch.from_numpy(g["x_start"]), torch.from_numpy(g["measurement"]),
+                            torch.from_numpy(g["step_noise"]), float(g["scale"]))
+    for k, (img, x0, sample, norm) in enumerate(traj):
+        scale = max(1.0, float(np.abs(g["img"][k]).max()))
+        assert np.abs(x0.numpy() - g["x0"][k]).max() < 2e-5 * scale, k
+        assert np.abs(sample.numpy() - g["sample"][k]).max() < 2e-5 * scale, k
+        assert np.abs(img.numpy() - g["img"][k]).max() < 2e-5 * scale, k
+        assert abs(float(norm) - g["dist"][k]) < 1e-5 * max(1.0, g["dist"][k]), k
+    assert np.abs(traj[-1][0].numpy() - g["out"]).max() < 2e-5 * max(1.0, float(np.abs(g["out"]).max()))
