@@ -77,4 +77,23 @@ __device__ __forceinline__ float sin_cw(float x) {
     return fabsf(x) < 39000.0f ? v : __builtin_amdgcn_sinf(x * 0.159154943091895335768f);
 }
 
+// fp32 cosine, same scheme (SLEEF cosf_u35 reduction): x = r + q*pi/2 with q odd,
+// cos(x) = -+sin(r); hardware v_cos_f32 beyond |x| >= 39000.
+__device__ __forceinline__ float cos_cw(float x) {
+    const float q = fmaf(2.0f, rintf(fmaf(x, 0.318309886183790671538f, -0.5f)), 1.0f);
+    float r = fmaf(q, -1.5703125f, x);
+    r = fmaf(q, -0.00048351287841796875f, r);
+    r = fmaf(q, -3.13855707645416259765625e-07f, r);
+    r = fmaf(q, -6.077100628276710381e-11f, r);
+    const float s = r * r;
+    float u = 2.6083159809786593541503e-06f;
+    u = fmaf(u, s, -0.0001981069071916863322258f);
+    u = fmaf(u, s, 0.00833307858556509017944336f);
+    u = fmaf(u, s, -0.166666597127914428710938f);
+    const float y = fmaf(s, u * r, r);
+    const unsigned sgn = ((unsigned)(int)q & 2u) ? 0u : (1u << 31);  // q = 1 mod 4: -sin(r)
+    const float v = __uint_as_float(__float_as_uint(y) ^ sgn);
+    return fabsf(x) < 39000.0f ? v : __builtin_amdgcn_cosf(x * 0.159154943091895335768f);
+}
+
 }  // namespace cfd

@@ -236,178 +236,264 @@ __global__ void siren_film(const float* __restrict__ V, const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Input-gradient (DPS adjoint): d<g, A(z)>/dz for the
+// Latent gradient (DPS adjoint): d<g, A(z)>/dz for the
 // Case4 measurement operator A = y_norm.denormalize(SIREN(x_norm(sensors), z))
-// (measurements.py:219-226).  One workgroup per latent row z, all sensors of the
-// row in groups of VJP_SG; thread j owns hidden feature j.  Sensor counts are
-// small (10 in the Case4 notebook), so this is VALU work on L2-resident weights:
-//   siren_tape_fwd  u_i = W_i x_i + F_i kept for every layer (the tape), x_{i+1} =
-//                   sin(w0 u_i); outputs A (coalesced W^T reads, x broadcast from LDS);
-//   siren_tape_vjp  delta_i = (W_{i+1}^T delta_{i+1}) * w0 cos(w0 u_i), summed over
-//                   sensors per layer, then g_z = sum_i V_i^T (sum_s delta_i).
+// (measurements.py:219-226).  The P = R x Ns (latent row, sensor) pairs are the
+// "coordinates" of the fused decoder's MFMA chain, each lane carrying its own
+// row's FiLM vectors:
+//   siren_tape_fwd  forward as siren_fused, also writing every layer's
+//                   pre-activation u_i (the tape) and the output A;
+//   siren_tape_bwd  delta_nh = (W_out^T g) * w0 cos(w0 u_nh), then
+//                   delta_{i-1} = (W_i^T delta_i) * w0 cos(w0 u_{i-1}) on MFMA with a
+//                   transposed weight image streamed in reverse layer order;
+//                   every delta_i is written out;
+//   siren_latent_grad  g_z[r] = sum_i V_i^T (sum_s delta_i[r, s]) in a fixed order
+//                   (deterministic, batch invariant).
 // ---------------------------------------------------------------------------
-constexpr int VJP_SG = 8;
-
-struct SirenVjpArgs {
-    const float* w0;     // (H, d)
-    const float* wtr;    // (nh, H, H) hidden weights transposed: wtr[i][k][j] = W_{i+1}[j][k]
-    const float* wraw;   // (nh, H, H) hidden weights as stored: W_{i+1}[j][k]
-    const float* wout;   // (c, H)
-    const float* bout;   // (c)
-    const float* V;      // (nh+1, H, L)
-    const float* film;   // (R, nh+1, H)
-    const float* coords; // (Ns, d) raw sensor coordinates
+struct SirenTapeArgs {
+    const float* w0;      // (H, d)
+    const float* wimg;    // forward weight image (as SirenArgs)
+    const float* wimg_t;  // transposed image, layers nh..1: img[j][q][lane][s] = W_i[16q+4g+s][16j+(lane&15)]
+    const float* wout;    // (c, H)
+    const float* bout;    // (c)
+    const float* film;    // (R, nh+1, H)
+    const float* coords;  // (Ns, d)
     const float* xmax;
     const float* xmin;
     const float* ymax;
     const float* ymin;
-    float* pre;          // (R, Ns, nh+1, H) tape
-    float* out;          // (R, Ns, c)  forward output A
-    const float* gout;   // (R, Ns, c)  gradient w.r.t. A
-    float* gz;           // (R, L)
+    float* u;             // (P, nh+1, H) tape
+    float* delta;         // (P, nh+1, H)
+    float* out;           // (P, c)
+    const float* gout;    // (P, c)
+    int64_t P;
     int64_t ystride;
-    int Ns, d, c, nh, H, L;
+    int Ns, d, c, nh;
     float w0f;
 };
 
-__global__ __launch_bounds__(512) void siren_tape_fwd(SirenVjpArgs p) {
-    extern __shared__ __attribute__((aligned(16))) float xs[];  // VJP_SG x H
-    const int64_t r = blockIdx.x;
-    const int j = threadIdx.x;
-    const int H = p.H, nl = p.nh + 1;
-    const float* film = p.film + r * nl * H;
-    for (int s0 = 0; s0 < p.Ns; s0 += VJP_SG) {
-        const int ns = min(VJP_SG, p.Ns - s0);
-        float* pre = p.pre + ((r * p.Ns + s0) * nl) * (int64_t)H;
-        if (j < H) {
-            const float f0 = film[j];
+template <int NB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void siren_tape_fwd(SirenTapeArgs p) {
+    constexpr int TILE = 16 * WAVES;
+    constexpr int H = NB * 16;
+    constexpr int BLK = NB * 256;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* wbuf = smem;
+    float* w0s = smem + 2 * BLK;  // (H, 4)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * TILE + wave * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int64_t row = nc / p.Ns;
+    const int sensor = (int)(nc - row * p.Ns);
+    const int nh = p.nh, nl = nh + 1;
+    const float* film = p.film + row * nl * H;
+    float* ut = p.u + nc * nl * H;
+    const bool live = n < p.P;
+
+    for (int f = threadIdx.x; f < H; f += 64 * WAVES) {
+        f4 w = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < p.d; ++k) w[k] = p.w0[f * p.d + k];
+        *(f4*)(w0s + 4 * f) = w;
+    }
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < VJP_SG; ++s) {
-                if (s < ns) {
-                    float a = 0.f;
-                    for (int k = 0; k < p.d; ++k) {
-                        float v = p.coords[(int64_t)(s0 + s) * p.d + k];
-                        if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
-                        a = k == 0 ? v * p.w0[j * p.d] : fmaf(v, p.w0[j * p.d + k], a);
-                    }
-                    const float u = a + f0;
-                    pre[(int64_t)s * nl * H + j] = u;
-                    xs[s * H + j] = sin_cw(p.w0f * u);
-                }
-            }
+    for (int k = 0; k < 4; ++k) {
+        if (k < p.d) {
+            float v = p.coords[(int64_t)sensor * p.d + k];
+            if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+            cn[k] = v;
         }
-        __syncthreads();
-        for (int i = 1; i <= p.nh; ++i) {
-            float acc[VJP_SG];
-            if (j < H) {
-                const float fi = film[i * H + j];
+    }
+    __syncthreads();
+    if (nh > 0) siren_issue_block<NB, WAVES>(p.wimg, 0, wbuf, wave, lane);
+
+    float X[NB][4];
+    static_for<NB>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
+        f4 uu;
 #pragma unroll
-                for (int s = 0; s < VJP_SG; ++s) acc[s] = fi;
-                const float* wt = p.wtr + (int64_t)(i - 1) * H * H + j;
-                for (int k = 0; k < H; ++k) {
-                    const float w = wt[(int64_t)k * H];
+        for (int r = 0; r < 4; ++r) {
+            const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
+            float a = cn[0] * w[0];
 #pragma unroll
-                    for (int s = 0; s < VJP_SG; ++s)
-                        if (s < ns) acc[s] = fmaf(w, xs[s * H + k], acc[s]);
-                }
-            }
+            for (int k = 1; k < 4; ++k)
+                if (k < p.d) a = fmaf(cn[k], w[k], a);
+            uu[r] = a + fv[r];
+            X[q][r] = sin_cw(p.w0f * uu[r]);
+        }
+        if (live) *(f4*)(ut + 16 * q + 4 * g) = uu;
+    });
+
+    const int nblocks = nh * NB;
+    int J = 0;
+    for (int layer = 1; layer <= nh; ++layer) {
+        f4 acc[NB];
+        static_for<NB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (J + 1 < nblocks) siren_issue_block<NB, WAVES>(p.wimg, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            const float* wb = wbuf + (J & 1) * BLK;
+            f4 a = *(const f4*)(film + layer * H + 16 * j + 4 * g);
+            static_for<NB>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                const f4 w = *(const f4*)(wb + (q * 64 + lane) * 4);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, X[q][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, X[q][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, X[q][2], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, X[q][3], a, 0, 0, 0);
+            });
+            acc[j] = a;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (j < H) {
+            ++J;
+        });
+        static_for<NB>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if (live) *(f4*)(ut + layer * H + 16 * q + 4 * g) = acc[q];
 #pragma unroll
-                for (int s = 0; s < VJP_SG; ++s) {
-                    if (s < ns) {
-                        pre[((int64_t)s * nl + i) * H + j] = acc[s];
-                        xs[s * H + j] = sin_cw(p.w0f * acc[s]);
-                    }
-                }
-            }
-            __syncthreads();
+            for (int r = 0; r < 4; ++r) X[q][r] = sin_cw(p.w0f * acc[q][r]);
+        });
+    }
+
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            const float* wr = p.wout + oc * H + 4 * g;
+            float s = 0.f;
+            static_for<NB>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                const f4 w = *(const f4*)(wr + 16 * q);
+                s = fmaf(w.x, X[q][0], s);
+                s = fmaf(w.y, X[q][1], s);
+                s = fmaf(w.z, X[q][2], s);
+                s = fmaf(w.w, X[q][3], s);
+            });
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            o[oc] = s + p.bout[oc];
         }
-        if (j < ns * p.c) {
-            const int s = j / p.c, oc = j - s * p.c;
-            float o = 0.f;
-            for (int k = 0; k < H; ++k) o = fmaf(p.wout[oc * H + k], xs[s * H + k], o);
-            o += p.bout[oc];
-            if (p.ymax) {
-                const int64_t yi = (int64_t)(s0 + s) * p.ystride + oc;
-                o = (o + 1.0f) / 2.0f * (p.ymax[yi] - p.ymin[yi]) + p.ymin[yi];
-            }
-            p.out[(r * p.Ns + s0 + s) * p.c + oc] = o;
+    }
+    if (live && g < p.c) {
+        float v = g == 0 ? o[0] : g == 1 ? o[1] : g == 2 ? o[2] : o[3];
+        if (p.ymax) {
+            const int64_t yi = (int64_t)sensor * p.ystride + g;
+            const float hi = p.ymax[yi], lo = p.ymin[yi];
+            v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
         }
-        __syncthreads();
+        p.out[n * p.c + g] = v;
     }
 }
 
-__global__ __launch_bounds__(512) void siren_tape_vjp(SirenVjpArgs p) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int64_t r = blockIdx.x;
-    const int j = threadIdx.x;
-    const int H = p.H, nl = p.nh + 1;
-    float* dl = sm;                   // VJP_SG x H: this layer's deltas
-    float* dacc = sm + VJP_SG * H;    // nl x H: deltas summed over sensors
-    for (int i = j; i < nl * H; i += blockDim.x) dacc[i] = 0.f;
-    for (int s0 = 0; s0 < p.Ns; s0 += VJP_SG) {
-        const int ns = min(VJP_SG, p.Ns - s0);
-        const float* pre = p.pre + ((r * p.Ns + s0) * nl) * (int64_t)H;
-        // gradient w.r.t. the last hidden activation: W_out^T (g * dA/dout)
-        float gx[VJP_SG];
+template <int NB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void siren_tape_bwd(SirenTapeArgs p) {
+    constexpr int TILE = 16 * WAVES;
+    constexpr int H = NB * 16;
+    constexpr int BLK = NB * 256;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* wbuf = smem;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * TILE + wave * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int sensor = (int)(nc % p.Ns);
+    const int nh = p.nh, nl = nh + 1;
+    const float* ut = p.u + nc * nl * H;
+    float* dt = p.delta + nc * nl * H;
+    const bool live = n < p.P;
+    const float w0f = p.w0f;
+
+    if (nh > 0) siren_issue_block<NB, WAVES>(p.wimg_t, 0, wbuf, wave, lane);
+    // gradient w.r.t. the raw output: g * (ymax - ymin) / 2 (denormalize), then
+    // delta_nh = (W_out^T dy) * w0 cos(w0 u_nh) in the B-operand layout
+    float dy[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < VJP_SG; ++s) gx[s] = 0.f;
-        if (j < H) {
-#pragma unroll
-            for (int s = 0; s < VJP_SG; ++s) {
-                if (s < ns) {
-                    float a = 0.f;
-                    for (int oc = 0; oc < p.c; ++oc) {
-                        float gy = p.gout[(r * p.Ns + s0 + s) * p.c + oc];
-                        if (p.ymax) {
-                            const int64_t yi = (int64_t)(s0 + s) * p.ystride + oc;
-                            gy = gy * ((p.ymax[yi] - p.ymin[yi]) / 2.0f);
-                        }
-                        a = fmaf(p.wout[oc * H + j], gy, a);
-                    }
-                    gx[s] = a;
-                }
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            float v = live ? p.gout[nc * p.c + oc] : 0.f;
+            if (p.ymax) {
+                const int64_t yi = (int64_t)sensor * p.ystride + oc;
+                v = v * ((p.ymax[yi] - p.ymin[yi]) / 2.0f);
             }
-        }
-        for (int i = p.nh; i >= 0; --i) {
-            if (j < H) {
-                float sum = 0.f;
-#pragma unroll
-                for (int s = 0; s < VJP_SG; ++s) {
-                    if (s < ns) {
-                        const float u = pre[((int64_t)s * nl + i) * H + j];
-                        const float dlt = gx[s] * (p.w0f * cosf(p.w0f * u));
-                        dl[s * H + j] = dlt;
-                        sum += dlt;
-                    }
-                }
-                dacc[i * H + j] += sum;
-            }
-            __syncthreads();
-            if (i > 0 && j < H) {
-                // gx = W_i^T delta_i  (W_i = hidden layer i, stored at slot i-1)
-#pragma unroll
-                for (int s = 0; s < VJP_SG; ++s) gx[s] = 0.f;
-                const float* w = p.wraw + (int64_t)(i - 1) * H * H + j;
-                for (int k = 0; k < H; ++k) {
-                    const float wv = w[(int64_t)k * H];
-#pragma unroll
-                    for (int s = 0; s < VJP_SG; ++s)
-                        if (s < ns) gx[s] = fmaf(wv, dl[s * H + k], gx[s]);
-                }
-            }
-            __syncthreads();
+            dy[oc] = v;
         }
     }
-    // g_z[l] = sum_i sum_f V_i[f][l] dacc[i][f]
-    for (int l = j; l < p.L; l += blockDim.x) {
-        float a = 0.f;
-        for (int i = 0; i < nl; ++i) {
-            const float* v = p.V + (int64_t)i * H * p.L + l;
-            for (int f = 0; f < H; ++f) a = fmaf(v[(int64_t)f * p.L], dacc[i * H + f], a);
+    float X[NB][4];
+    static_for<NB>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        const f4 uu = *(const f4*)(ut + nh * H + 16 * q + 4 * g);
+        f4 dd;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = 16 * q + 4 * g + r;
+            float gx = 0.f;
+#pragma unroll
+            for (int oc = 0; oc < 4; ++oc)
+                if (oc < p.c) gx = fmaf(p.wout[oc * H + f], dy[oc], gx);
+            dd[r] = gx * (w0f * cos_cw(w0f * uu[r]));
+            X[q][r] = dd[r];
         }
-        p.gz[r * p.L + l] = a;
+        if (live) *(f4*)(dt + nh * H + 16 * q + 4 * g) = dd;
+    });
+
+    const int nblocks = nh * NB;
+    int J = 0;
+    for (int layer = nh; layer >= 1; --layer) {
+        // delta_{layer-1} = (W_layer^T delta_layer) * w0 cos(w0 u_{layer-1})
+        f4 acc[NB];
+        static_for<NB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (J + 1 < nblocks)
+                siren_issue_block<NB, WAVES>(p.wimg_t, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            const float* wb = wbuf + (J & 1) * BLK;
+            f4 a = {0.f, 0.f, 0.f, 0.f};
+            static_for<NB>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                const f4 w = *(const f4*)(wb + (q * 64 + lane) * 4);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, X[q][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, X[q][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, X[q][2], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, X[q][3], a, 0, 0, 0);
+            });
+            acc[j] = a;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            ++J;
+        });
+        const int li = layer - 1;
+        static_for<NB>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const f4 uu = *(const f4*)(ut + li * H + 16 * q + 4 * g);
+            f4 dd;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                dd[r] = acc[q][r] * (w0f * cos_cw(w0f * uu[r]));
+                X[q][r] = dd[r];
+            }
+            if (live) *(f4*)(dt + li * H + 16 * q + 4 * g) = dd;
+        });
+    }
+}
+
+// g_z[r][l] = sum_i sum_f V_i[f][l] * (sum_s delta[r*Ns + s][i][f])
+__global__ __launch_bounds__(256) void siren_latent_grad(const float* __restrict__ delta,
+                                                         const float* __restrict__ V, float* __restrict__ gz,
+                                                         int Ns, int nl, int H, int L) {
+    extern __shared__ __attribute__((aligned(16))) float D[];  // nl * H
+    const int64_t r = blockIdx.x;
+    const int nf = nl * H;
+    const float* dr = delta + r * (int64_t)Ns * nf;
+    for (int i = threadIdx.x; i < nf; i += blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < Ns; ++k) s += dr[(int64_t)k * nf + i];
+        D[i] = s;
+    }
+    __syncthreads();
+    for (int l = threadIdx.x; l < L; l += blockDim.x) {
+        float a = 0.f;
+        for (int i = 0; i < nf; ++i) a = fmaf(V[(int64_t)i * L + l], D[i], a);
+        gz[r * L + l] = a;
     }
 }
 
@@ -433,8 +519,7 @@ struct cfd_siren {
     float* wimg = nullptr;  // nh * NB * NB*256
     float* wout = nullptr;  // (c, H)
     float* bout = nullptr;  // (c)
-    float* wraw = nullptr;  // (nh, H, H) hidden weights (input-gradient path)
-    float* wtr = nullptr;   // (nh, H, H) hidden weights transposed
+    float* wimg_t = nullptr; // transposed weight image, layers nh..1 (latent-gradient path)
 };
 
 namespace {
@@ -521,8 +606,7 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_HIP(hipMalloc(&h->wimg, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wout, sizeof(float) * c * H));
         CFD_HIP(hipMalloc(&h->bout, sizeof(float) * 4));
-        CFD_HIP(hipMalloc(&h->wraw, sizeof(float) * (size_t)std::max(nh, 1) * H * H));
-        CFD_HIP(hipMalloc(&h->wtr, sizeof(float) * (size_t)std::max(nh, 1) * H * H));
+        CFD_HIP(hipMalloc(&h->wimg_t, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         *out = h;
     });
 }
@@ -535,8 +619,7 @@ extern "C" void cfd_siren_destroy(cfd_siren* h) {
     (void)hipFree(h->wimg);
     (void)hipFree(h->wout);
     (void)hipFree(h->bout);
-    (void)hipFree(h->wraw);
-    (void)hipFree(h->wtr);
+    (void)hipFree(h->wimg_t);
     delete h;
 }
 
@@ -595,11 +678,16 @@ extern "C" int cfd_siren_set_param(cfd_siren* h, const char* key, const float* h
                                 host[(size_t)(16 * j + (lane & 15)) * H + 16 * q + 4 * (lane >> 4) + s];
             CFD_HIP(hipMemcpy(h->wimg + (size_t)(li - 1) * NB * NB * 256, img.data(), img.size() * 4,
                               hipMemcpyHostToDevice));
-            std::vector<float> tr((size_t)H * H);
-            for (int a = 0; a < H; ++a)
-                for (int bb = 0; bb < H; ++bb) tr[(size_t)bb * H + a] = host[(size_t)a * H + bb];
-            CFD_HIP(hipMemcpy(h->wraw + (size_t)(li - 1) * H * H, host, n * 4, hipMemcpyHostToDevice));
-            CFD_HIP(hipMemcpy(h->wtr + (size_t)(li - 1) * H * H, tr.data(), n * 4, hipMemcpyHostToDevice));
+            // transposed image for the backward chain, stored at slot nh - li:
+            // img_t[j][q][lane][s] = W[16q + 4(lane>>4) + s][16j + (lane&15)]
+            for (int j = 0; j < NB; ++j)
+                for (int q = 0; q < NB; ++q)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int s2 = 0; s2 < 4; ++s2)
+                            img[(((size_t)j * NB + q) * 64 + lane) * 4 + s2] =
+                                host[(size_t)(16 * q + 4 * (lane >> 4) + s2) * H + 16 * j + (lane & 15)];
+            CFD_HIP(hipMemcpy(h->wimg_t + (size_t)(nh - li) * NB * NB * 256, img.data(), img.size() * 4,
+                              hipMemcpyHostToDevice));
         }
         (void)c;
         prm->set = true;
@@ -661,26 +749,66 @@ extern "C" int cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, c
 
 namespace {
 
-void siren_vjp_args(const cfd_siren* h, cfd::SirenVjpArgs& a, int64_t Ns, int R, void* ws) {
+void tape_args(const cfd_siren* h, cfd::SirenTapeArgs& a, int64_t Ns, int R, void* ws) {
     const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features;
+    const size_t nl = nh + 1;
     a.w0 = h->w0;
-    a.wtr = h->wtr;
-    a.wraw = h->wraw;
+    a.wimg = h->wimg;
+    a.wimg_t = h->wimg_t;
     a.wout = h->wout;
     a.bout = h->bout;
-    a.V = h->V;
     a.film = (float*)ws;
-    a.pre = (float*)ws + (size_t)R * (nh + 1) * H;
+    a.u = (float*)ws + (size_t)R * nl * H;
+    a.delta = a.u + (size_t)R * Ns * nl * H;
+    a.P = (int64_t)R * Ns;
     a.Ns = (int)Ns;
     a.d = h->cfg.in_coord_features;
     a.c = h->cfg.out_features;
     a.nh = nh;
-    a.H = H;
-    a.L = h->cfg.in_latent_features;
     a.w0f = h->cfg.w0;
 }
 
-int vjp_threads(int H) { return (H + 63) / 64 * 64; }
+// waves per workgroup: 4 when there are enough pairs to fill the chip, else fewer
+// (the pair count of a DPS step is small: R * Ns = B * T * 10)
+int tape_waves(int64_t P) { return P >= 16 * 4 * 512 ? 4 : P >= 16 * 2 * 256 ? 2 : 1; }
+
+template <int NB, int W>
+void launch_tape_w(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
+    const size_t lds = sizeof(float) * (2 * NB * 256 + (bwd ? 0 : 4 * NB * 16));
+    const void* fn = bwd ? (const void*)cfd::siren_tape_bwd<NB, W> : (const void*)cfd::siren_tape_fwd<NB, W>;
+    CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const dim3 grid((unsigned)cfd::ceil_div(a.P, 16 * W));
+    if (bwd)
+        hipLaunchKernelGGL((cfd::siren_tape_bwd<NB, W>), grid, dim3(64 * W), lds, st, a);
+    else
+        hipLaunchKernelGGL((cfd::siren_tape_fwd<NB, W>), grid, dim3(64 * W), lds, st, a);
+    cfd::check_launch(bwd ? "siren_tape_bwd" : "siren_tape_fwd");
+}
+
+template <int NB>
+void launch_tape_nb(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
+    switch (tape_waves(a.P)) {
+        case 4: return launch_tape_w<NB, 4>(a, bwd, st);
+        case 2: return launch_tape_w<NB, 2>(a, bwd, st);
+        default: return launch_tape_w<NB, 1>(a, bwd, st);
+    }
+}
+
+void launch_tape(const cfd_siren* h, const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
+    switch (h->NB) {
+        case 1: return launch_tape_nb<1>(a, bwd, st);
+        case 2: return launch_tape_nb<2>(a, bwd, st);
+        case 3: return launch_tape_nb<3>(a, bwd, st);
+        case 4: return launch_tape_nb<4>(a, bwd, st);
+        case 6: return launch_tape_nb<6>(a, bwd, st);
+        case 8: return launch_tape_nb<8>(a, bwd, st);
+        case 12: return launch_tape_nb<12>(a, bwd, st);
+        case 16: return launch_tape_nb<16>(a, bwd, st);
+        case 24: return launch_tape_nb<24>(a, bwd, st);
+        case 32: return launch_tape_nb<32>(a, bwd, st);
+        default: throw cfd::Error{CFD_EARG, "hidden_features must be 16*{1,2,3,4,6,8,12,16,24,32}"};
+    }
+}
 
 }  // namespace
 
@@ -688,7 +816,7 @@ extern "C" int cfd_siren_vjp_workspace_bytes(const cfd_siren* h, int64_t Ns, int
     return cfd::guard([&] {
         CFD_REQUIRE(h && bytes && Ns >= 0 && R >= 0, CFD_EARG, "bad argument");
         const size_t nl = h->cfg.num_hidden_layers + 1, H = h->cfg.hidden_features;
-        *bytes = sizeof(float) * ((size_t)R * nl * H + (size_t)R * Ns * nl * H);
+        *bytes = sizeof(float) * ((size_t)R * nl * H + 2 * (size_t)R * Ns * nl * H);
     });
 }
 
@@ -700,13 +828,14 @@ extern "C" int cfd_siren_tape_forward(cfd_siren* h, const float* coords, int64_t
         CFD_REQUIRE(Ns >= 1 && Ns <= (1 << 20) && R >= 1, CFD_EARG, "bad sensor / row count");
         CFD_REQUIRE((xmax == nullptr) == (xmin == nullptr) && (ymax == nullptr) == (ymin == nullptr), CFD_EARG,
                     "normaliser bounds must be set in pairs");
+        CFD_REQUIRE(((uintptr_t)ws & 15) == 0, CFD_EARG, "workspace must be 16-byte aligned");
         size_t need = 0;
         cfd_siren_vjp_workspace_bytes(h, Ns, R, &need);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
         const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features, L = h->cfg.in_latent_features;
         auto st = (hipStream_t)stream;
-        cfd::SirenVjpArgs a{};
-        siren_vjp_args(h, a, Ns, R, ws);
+        cfd::SirenTapeArgs a{};
+        tape_args(h, a, Ns, R, ws);
         a.coords = coords;
         a.xmax = xmax;
         a.xmin = xmin;
@@ -717,9 +846,7 @@ extern "C" int cfd_siren_tape_forward(cfd_siren* h, const float* coords, int64_t
         hipLaunchKernelGGL(cfd::siren_film, dim3(nh + 1, R), dim3(128), 0, st, h->V, h->fbias, latents, (float*)ws,
                            H, L, nh + 1);
         cfd::check_launch("siren_film");
-        hipLaunchKernelGGL(cfd::siren_tape_fwd, dim3(R), dim3(vjp_threads(H)), sizeof(float) * cfd::VJP_SG * H, st,
-                           a);
-        cfd::check_launch("siren_tape_fwd");
+        launch_tape(h, a, false, st);
     });
 }
 
@@ -733,19 +860,21 @@ extern "C" int cfd_siren_tape_vjp(cfd_siren* h, const float* g_out, int64_t Ns, 
         size_t need = 0;
         cfd_siren_vjp_workspace_bytes(h, Ns, R, &need);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features;
-        cfd::SirenVjpArgs a{};
-        siren_vjp_args(h, a, Ns, R, ws);
+        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features, L = h->cfg.in_latent_features;
+        auto st = (hipStream_t)stream;
+        cfd::SirenTapeArgs a{};
+        tape_args(h, a, Ns, R, ws);
         a.ymax = ymax;
         a.ymin = ymin;
         a.ystride = y_stride;
         a.gout = g_out;
-        a.gz = g_latents;
-        const size_t lds = sizeof(float) * ((size_t)cfd::VJP_SG * H + (size_t)(nh + 1) * H);
-        CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the input-gradient kernel");
-        CFD_HIP(hipFuncSetAttribute((const void*)cfd::siren_tape_vjp, hipFuncAttributeMaxDynamicSharedMemorySize,
+        launch_tape(h, a, true, st);
+        const size_t lds = sizeof(float) * (size_t)(nh + 1) * H;
+        CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the latent-gradient reduction");
+        CFD_HIP(hipFuncSetAttribute((const void*)cfd::siren_latent_grad, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
-        hipLaunchKernelGGL(cfd::siren_tape_vjp, dim3(R), dim3(vjp_threads(H)), lds, (hipStream_t)stream, a);
-        cfd::check_launch("siren_tape_vjp");
+        hipLaunchKernelGGL(cfd::siren_latent_grad, dim3(R), dim3(256), lds, st, a.delta, h->V, g_latents, (int)Ns,
+                           nh + 1, H, L);
+        cfd::check_launch("siren_latent_grad");
     });
 }

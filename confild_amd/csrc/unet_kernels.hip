@@ -575,7 +575,7 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     const int64_t mn = (int64_t)8 * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;
     auto tiles = [&](int bm) { return ceil_div(mn, bm) * ceil_div(a.Cout, p.bn); };
-    p.bm = force_bm ? force_bm : (p.bn == 128 ? 128 : 64);
+    p.bm = force_bm ? force_bm : 64;  // 64x128 measured ahead of 128x128 (r01 sweep: 8.76 vs 9.26 ms)
     const int nkt = a.K / 32;
     p.splits = 1;
     while (tiles(p.bm) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16) p.splits *= 2;

@@ -3,6 +3,7 @@
     python tools/kbench.py siren [--latents 64]      # config-B CNF decode
     python tools/kbench.py unet  [--batch 8]         # one U-Net forward
     python tools/kbench.py sweep                      # both, short
+    python tools/kbench.py dps   [--batch 8]         # one DPS step (config D) and its parts
 Prints one JSON line per measurement.
 """
 from __future__ import annotations
@@ -68,9 +69,51 @@ def bench_unet(batch=8, size=64, iters=10):
                       "tflops": batch * gf * 1e9 / (best / 1e3) / 1e12}), flush=True)
 
 
+def bench_dps(batch=8, size=64, ns=10, dims=(3, 64, 3, 15, 384), iters=5):
+    """Config D: one guided (DPS) reverse step of B chains and its components."""
+    import functools
+    from confild_amd.guided.condition_methods import get_conditioning_method
+    from confild_amd.guided.gaussian_diffusion import create_sampler
+    from confild_amd.guided.measurements import Case4Operator, get_noise
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    from confild_amd.normalize import Normalizer_ts
+    from confild_amd.script_util import create_model
+    m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                     attention_resolutions="32,16,8")
+    sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.to(DEV)
+    d, L, c, nh, H = dims
+    nf = SIRENAutodecoder_film(d, L, c, nh, H)
+    nf.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, d, L, c, nh, H).items()})
+    coords = torch.rand(ns, d)
+    xn = Normalizer_ts(params=(torch.ones(1, d), torch.zeros(1, d)), method="-11", dim=0)
+    yn = Normalizer_ts(params=(torch.ones(c), -torch.ones(c)), method="-11", dim=0)
+    op = Case4Operator.from_parts(DEV, coords, xn, yn, nf, torch.full((L,), 1.5), torch.full((L,), -1.5))
+    cond = get_conditioning_method(operator=op, noiser=get_noise(sigma=0.0, name="gaussian"), name="ps", scale=1.0)
+    smp = create_sampler(sampler="ddpm", steps=1000, noise_schedule="cosine", model_mean_type="epsilon",
+                         model_var_type="fixed_large", dynamic_threshold=False, clip_denoised=True,
+                         rescale_timesteps=False, timestep_respacing="256")
+    fn = functools.partial(cond.conditioning)
+    x = torch.randn(batch, 1, size, size, device=DEV)
+    y = torch.randn(size, ns, c, device=DEV)
+    t = torch.full((batch,), 500, dtype=torch.int64, device=DEV)
+    res = {"kernel": "dps_step", "batch": batch, "size": size, "sensors": ns}
+    res["step_ms"], _ = timeit(lambda: smp.p_sample_step(m, x, 128, y, fn, seed=1, counter=0), iters=iters, warm=2)
+    res["unet_fwd_ms"], _ = timeit(lambda: m(x, t), iters=iters)
+    res["unet_fwd_tape_ms"], _ = timeit(lambda: m.forward_tape(x, t), iters=iters)
+    de = torch.randn_like(x)
+    res["unet_vjp_ms"], _ = timeit(lambda: m.input_vjp(de), iters=iters)
+    x0 = x.clamp(-1, 1)
+    res["siren_tape_fwd_ms"], _ = timeit(lambda: op.forward_tape(x0), iters=iters)
+    g = torch.randn(batch * size, ns, c, device=DEV)
+    res["siren_vjp_ms"], _ = timeit(lambda: op.vjp(g), iters=iters)
+    print(json.dumps(res), flush=True)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["siren", "unet", "sweep"])
+    ap.add_argument("what", choices=["siren", "unet", "sweep", "dps"])
     ap.add_argument("--latents", type=int, default=64)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=64)
@@ -79,3 +122,5 @@ if __name__ == "__main__":
         bench_siren(a.latents)
     if a.what in ("unet", "sweep"):
         bench_unet(a.batch, a.size)
+    if a.what == "dps":
+        bench_dps(a.batch, a.size)
