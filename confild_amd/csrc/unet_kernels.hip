@@ -81,13 +81,26 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnArgs a) {
     const int64_t b = blockIdx.x;
     const int Ctot = a.Ctot, cpg = Ctot / 32;
     __shared__ float sh_mean[32], sh_rstd[32];
-    if (threadIdx.x < 32) {
-        const int grp = threadIdx.x;
+    __shared__ double red[2][256];
+    // 8 threads per group, each summing every 8th chunk; then a fixed-order combine
+    {
+        const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
         double s = 0, s2 = 0;
-        for (int ch = 0; ch < a.nchunks; ++ch) {
+        for (int ch = sub; ch < a.nchunks; ch += 8) {
             const double* src = a.part + ((b * a.nchunks + ch) * 32 + grp) * 2;
             s += src[0];
             s2 += src[1];
+        }
+        red[0][threadIdx.x] = s;
+        red[1][threadIdx.x] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        const int grp = threadIdx.x;
+        double s = 0, s2 = 0;
+        for (int k = 0; k < 8; ++k) {
+            s += red[0][grp * 8 + k];
+            s2 += red[1][grp * 8 + k];
         }
         const double n = (double)a.HW * cpg;
         const double mean = s / n;

@@ -81,19 +81,32 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnbArgs a) {
     }
 }
 
-__global__ void gn_bwd_finalize_kernel(GnbArgs a) {
+__global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(GnbArgs a) {
     const int64_t b = blockIdx.x;
-    const int grp = threadIdx.x;
-    if (grp >= 32) return;
-    double s = 0, s2 = 0;
-    for (int ch = 0; ch < a.nchunks; ++ch) {
-        const double* src = a.part + ((b * a.nchunks + ch) * 32 + grp) * 2;
-        s += src[0];
-        s2 += src[1];
+    __shared__ double red[2][256];
+    {
+        const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
+        double s = 0, s2 = 0;
+        for (int ch = sub; ch < a.nchunks; ch += 8) {
+            const double* src = a.part + ((b * a.nchunks + ch) * 32 + grp) * 2;
+            s += src[0];
+            s2 += src[1];
+        }
+        red[0][threadIdx.x] = s;
+        red[1][threadIdx.x] = s2;
     }
-    const double n = (double)a.HW * (a.Ctot / 32);
-    a.fin[(b * 32 + grp) * 2 + 0] = (float)(s / n);
-    a.fin[(b * 32 + grp) * 2 + 1] = (float)(s2 / n);
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        const int grp = threadIdx.x;
+        double s = 0, s2 = 0;
+        for (int k = 0; k < 8; ++k) {
+            s += red[0][grp * 8 + k];
+            s2 += red[1][grp * 8 + k];
+        }
+        const double n = (double)a.HW * (a.Ctot / 32);
+        a.fin[(b * 32 + grp) * 2 + 0] = (float)(s / n);
+        a.fin[(b * 32 + grp) * 2 + 1] = (float)(s2 / n);
+    }
 }
 
 __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(GnbArgs a) {
@@ -313,7 +326,7 @@ void launch_gn_bwd(const GnbArgs& a0, int B, hipStream_t st) {
     a.B = B;
     hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
     check_launch("gn_bwd_partial_kernel");
-    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B), dim3(256), 0, st, a);
     check_launch("gn_bwd_finalize_kernel");
     const int64_t nq = (int64_t)B * a.HW * a.Ctot / 4;
     hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a);
