@@ -39,6 +39,23 @@ FMA_PEAK_TFLOPS = 157.3   # MI355X fp32 matrix peak (MI355X_MICROARCH.md chip ta
 HBM_PEAK_GBS = 8000.0
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_siren_pmc.json")
+
+
+def measured_traffic(latents, npts):
+    """Per-launch fabric bytes of siren_fused from the committed rocprofv3 PMC
+    record (tools/pmc_traffic.py), scaled from its launch geometry to this one."""
+    try:
+        rec = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
+    launch = rec.get("launch", {})
+    ref_pairs = launch.get("latents", 0) * launch.get("coords", 0)
+    if not ref_pairs or "siren_fused" not in rec.get("kernel", ""):
+        return None
+    return rec["traffic_bytes_per_launch"] * (latents * npts) / ref_pairs
+
+
 def siren_flops_per_pair(d, L, c, nh, H):
     return 2 * (d * H + nh * H * H + H * c)
 
@@ -209,7 +226,8 @@ def main():
                        "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world} (independent batches)"},
             "roofline": {"bound": "mfma", "kernel": "siren_fused (+siren_film)", "achieved": achieved,
                          "peak": FMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FMA_PEAK_TFLOPS,
-                         "traffic": None, "flops_per_launch": flops, "launch_ms": dec_s * 1e3,
+                         "traffic": measured_traffic(B * S, GRID ** 3), "flops_per_launch": flops,
+                         "launch_ms": dec_s * 1e3,
                          "unet_share_ms": (elapsed / args.steps - dec_s) * 1e3},
             "cpu_baseline": cpu,
         }
