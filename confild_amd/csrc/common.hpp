@@ -9,6 +9,8 @@
 #include "../../include/confild.h"
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace cfd {
 

@@ -4,6 +4,7 @@
 // unet_kernels.hip.  All activations are NHWC fp32 in one caller-provided
 // workspace; the forward issues only kernel launches on the given stream.
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <map>
 #include <string>
@@ -63,6 +64,8 @@ struct cfd_unet {
     float* freqs = nullptr; // (mc/2) timestep-embedding frequencies
     float* arena_t = nullptr; // transposed conv weights (input-gradient path)
     size_t arena_t_floats = 0;
+    uint16_t* arena_bf = nullptr;  // bf16 copy of the conv weights, same offsets as arena
+    int compute = CFD_COMPUTE_F32;
 };
 
 namespace {
@@ -206,6 +209,22 @@ void build(cfd_unet* h) {
         toff += ((p.tpack == 2 ? p.count / 9 * 16 : p.count) + 3) & ~size_t(3);
     }
     h->arena_t_floats = toff;
+}
+
+// bf16 copy of a packed conv weight, or null in fp32 compute
+const void* PB(const cfd_unet* h, const std::string& key) {
+    if (h->compute != CFD_COMPUTE_BF16) return nullptr;
+    auto it = h->index.find(key);
+    CFD_REQUIRE(it != h->index.end(), CFD_EKEY, "internal: missing param " + key);
+    return h->arena_bf + h->params[it->second].offset;
+}
+
+// fp32 -> bf16, round to nearest even (what v_cvt_pk_bf16_f32 does on the device)
+uint16_t to_bf16(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
 const float* PT(const cfd_unet* h, const std::string& key) {
@@ -385,6 +404,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         a.C2 = in.Cb;
         a.Ctot = in.C();
         a.w = P(h, pre + ".weight");
+        a.wbf = PB(h, pre + ".weight");
         a.bias = P(h, pre + ".bias");
         a.emb = embp;
         a.emb_stride = h->emb_total;
@@ -744,6 +764,7 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             CFD_HIP(hipMalloc(&h->emb_w, sizeof(float) * (size_t)h->emb_total * h->tdim));
             CFD_HIP(hipMalloc(&h->emb_b, sizeof(float) * (size_t)h->emb_total));
             CFD_HIP(hipMalloc(&h->arena_t, sizeof(float) * std::max<size_t>(h->arena_t_floats, 4)));
+            CFD_HIP(hipMalloc(&h->arena_bf, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
             const int half = cfg->model_channels / 2;
             // freqs = exp(-ln(10000) * arange(half, fp32) / half) in fp32 (nn.py:129-131)
             std::vector<float> fr(half);
@@ -766,6 +787,7 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->emb_b);
     (void)hipFree(h->freqs);
     (void)hipFree(h->arena_t);
+    (void)hipFree(h->arena_bf);
     delete h;
 }
 
@@ -797,17 +819,23 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
         CFD_HIP(hipSetDevice(h->device));
         switch (p.pack) {
             case Pack::Raw:
-            case Pack::Conv1:
                 CFD_HIP(hipMemcpy(h->arena + p.offset, host, n * 4, hipMemcpyHostToDevice));
                 break;
+            case Pack::Conv1:
             case Pack::Conv3: {
-                // (Cout, Cin, 3, 3) -> (Cout, tap, Cin): GEMM K ordered (tap, channel)
-                const int64_t co = p.shape[0], ci = p.shape[1];
-                std::vector<float> pk(n);
-                for (int64_t o = 0; o < co; ++o)
-                    for (int64_t i = 0; i < ci; ++i)
-                        for (int tap = 0; tap < 9; ++tap) pk[(o * 9 + tap) * ci + i] = host[(o * ci + i) * 9 + tap];
+                // 3x3: (Cout, Cin, 3, 3) -> (Cout, tap, Cin): GEMM K ordered (tap, channel)
+                std::vector<float> pk(host, host + n);
+                if (p.pack == Pack::Conv3) {
+                    const int64_t co = p.shape[0], ci = p.shape[1];
+                    for (int64_t o = 0; o < co; ++o)
+                        for (int64_t i = 0; i < ci; ++i)
+                            for (int tap = 0; tap < 9; ++tap)
+                                pk[(o * 9 + tap) * ci + i] = host[(o * ci + i) * 9 + tap];
+                }
                 CFD_HIP(hipMemcpy(h->arena + p.offset, pk.data(), n * 4, hipMemcpyHostToDevice));
+                std::vector<uint16_t> bf(n);
+                for (size_t e = 0; e < n; ++e) bf[e] = to_bf16(pk[e]);
+                CFD_HIP(hipMemcpy(h->arena_bf + p.offset, bf.data(), n * 2, hipMemcpyHostToDevice));
                 break;
             }
             case Pack::EmbW:
@@ -847,6 +875,14 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
             CFD_HIP(hipMemcpy(h->arena_t + p.toffset, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
         }
         p.set = true;
+    });
+}
+
+extern "C" int cfd_unet_set_compute(cfd_unet* h, int compute) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h, CFD_EARG, "null handle");
+        CFD_REQUIRE(compute == CFD_COMPUTE_F32 || compute == CFD_COMPUTE_BF16, CFD_EARG, "unknown compute mode");
+        h->compute = compute;
     });
 }
 
@@ -920,6 +956,8 @@ extern "C" int cfd_unet_forward_tape(cfd_unet* h, const float* x, const int64_t*
                                      void* workspace, size_t ws_bytes, void* tape, size_t tape_bytes, void* stream) {
     return cfd::guard([&] {
         CFD_REQUIRE(h && x && t && eps && workspace && tape, CFD_EARG, "null argument");
+        CFD_REQUIRE(h->compute == CFD_COMPUTE_F32, CFD_ESTATE,
+                    "the input-gradient path is fp32: call cfd_unet_set_compute(h, CFD_COMPUTE_F32) first");
         CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
         check_ready(h);
         size_t need = 0, tneed = 0;

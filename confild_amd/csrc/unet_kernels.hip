@@ -162,14 +162,22 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 32 + 4 * (chunk ^ ((row ^ (row >> 1)) & 7)); }
 
-template <int BM, int BN, bool TMODE>
+// BF (config E): bf16 operands, fp32 accumulate on v_mfma_f32_16x16x32_bf16.  The
+// fp32 activations are rounded to bf16 (RNE, v_cvt_pk_bf16_f32) as the A tile is
+// staged; weights come pre-rounded (a.wbf).  An LDS row is 32 bf16 = four 16-B
+// chunks, chunk c of row r stored at ((c + (r>>2)) & 3): one ds_read_b128 per lane
+// (k = 8g..8g+7, the MFMA operand layout), conflict-free.
+__device__ __forceinline__ int lds_swz_bf(int row, int chunk) { return row * 64 + ((chunk + (row >> 2)) & 3) * 16; }
+
+template <int BM, int BN, bool TMODE, bool BF>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     constexpr int BK = 32;
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 16, TN = WN / 16;
-    constexpr int AIT = BM / 32, BIT = BN / 32;  // float4 per thread per tile
-    __shared__ __attribute__((aligned(16))) float As[2][BM * BK];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN * BK];
+    constexpr int AIT = BM / 32, BIT = BN / 32;  // float4 (bf16: 4 x bf16) per thread per tile
+    constexpr int AFL = BF ? BM * BK / 2 : BM * BK, BFL = BF ? BN * BK / 2 : BN * BK;
+    __shared__ __attribute__((aligned(16))) float As[2][AFL];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BFL];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -200,12 +208,16 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         }
     }
     const float* wrow[BIT];
+    const unsigned short* wrow_bf[BIT];
     bool b_ok[BIT];
 #pragma unroll
     for (int it = 0; it < BIT; ++it) {
         const int n = n0 + rsub + it * 32;
         b_ok[it] = n < a.Cout;
-        wrow[it] = a.w + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
+        if constexpr (BF)
+            wrow_bf[it] = (const unsigned short*)a.wbf + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
+        else
+            wrow[it] = a.w + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
     }
     const int nkt = a.K / BK;
     const int per = (nkt + gridDim.z - 1) / gridDim.z;
@@ -223,6 +235,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
 
     const int smask = a.stride - 1, sshift = a.stride >> 1;
     f4 ra[AIT], rb[BIT];
+    uint2 rbh[BIT];
     auto load_tile = [&](int kt) {
         const int c0 = cb + 4 * kq;
 #pragma unroll
@@ -256,8 +269,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
             ra[it] = v;
         }
 #pragma unroll
-        for (int it = 0; it < BIT; ++it)
-            rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kt * BK) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int it = 0; it < BIT; ++it) {
+            if constexpr (BF)
+                rbh[it] = b_ok[it] ? *(const uint2*)(wrow_bf[it] + kt * BK) : uint2{0u, 0u};
+            else
+                rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kt * BK) : f4{0.f, 0.f, 0.f, 0.f};
+        }
         cb += BK;
         if (cb >= a.Ctot) {
             cb = 0;
@@ -268,10 +285,22 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         }
     };
     auto store_tile = [&](int buf) {
+        if constexpr (BF) {
+            // thread kq holds k = 4kq..4kq+3: chunk kq/2, half kq%2
 #pragma unroll
-        for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][lds_swz(rsub + it * 32, kq)]) = ra[it];
+            for (int it = 0; it < AIT; ++it) {
+                const bf16x4 v = __builtin_convertvector(ra[it], bf16x4);
+                *(bf16x4*)((char*)As[buf] + lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8) = v;
+            }
 #pragma unroll
-        for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][lds_swz(rsub + it * 32, kq)]) = rb[it];
+            for (int it = 0; it < BIT; ++it)
+                *(uint2*)((char*)Bs[buf] + lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8) = rbh[it];
+        } else {
+#pragma unroll
+            for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][lds_swz(rsub + it * 32, kq)]) = ra[it];
+#pragma unroll
+            for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][lds_swz(rsub + it * 32, kq)]) = rb[it];
+        }
     };
 
     f4 acc[TM][TN];
@@ -288,6 +317,21 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         for (int kt = kt0; kt < kt1; ++kt) {
             const int cur = (kt - kt0) & 1;
             if (kt + 1 < kt1) load_tile(kt + 1);
+            if constexpr (BF) {
+                const int g = lane >> 4;
+                bf16x8 fa[TM], fb[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    fa[i] = *(const bf16x8*)((const char*)As[cur] + lds_swz_bf(wm * WM + 16 * i + li, g));
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    fb[j] = *(const bf16x8*)((const char*)Bs[cur] + lds_swz_bf(wn * WN + 16 * j + li, g));
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            } else
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 f4 fa[TM], fb[TN];
@@ -598,16 +642,16 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     return p;
 }
 
-template <bool TMODE>
+template <bool TMODE, bool BF>
 static void launch_conv_tiles(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
     if (p.bm == 128 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, BF>), grid, dim3(256), 0, st, a);
     else if (p.bm == 64 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE, BF>), grid, dim3(256), 0, st, a);
     else if (p.bm == 128 && p.bn == 64)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 64, TMODE>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 64, TMODE, BF>), grid, dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE, BF>), grid, dim3(256), 0, st, a);
 }
 
 void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
@@ -616,10 +660,13 @@ void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
     CFD_REQUIRE(!a.tmode || ((a.stride == 1 || a.stride == 2) && !a.up), CFD_ESHAPE, "transposed conv: stride 1|2");
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
+    CFD_REQUIRE(!(a.tmode && a.wbf), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
     if (a.tmode)
-        launch_conv_tiles<true>(a, p, grid, st);
+        launch_conv_tiles<true, false>(a, p, grid, st);
+    else if (a.wbf)
+        launch_conv_tiles<false, true>(a, p, grid, st);
     else
-        launch_conv_tiles<false>(a, p, grid, st);
+        launch_conv_tiles<false, false>(a, p, grid, st);
     check_launch("conv_gemm_kernel");
     if (p.splits > 1) {
         const int64_t total4 = (int64_t)a.M * a.Cout / 4;

@@ -174,6 +174,7 @@ class UNetModel(nn.Module):
         self._shapes = shapes
         _build_tree(self, shapes)
         self._reset_parameters()
+        self.compute = "fp32"  # convolution operands: "fp32" (reference arithmetic) or "bf16" (config E)
         self._handles = {}      # device index -> (handle ptr, uploaded signature)
         self._workspaces = {}   # (device, B) -> uint8 tensor
 
@@ -215,6 +216,14 @@ class UNetModel(nn.Module):
         cfg.num_head_channels = self.num_head_channels
         return cfg
 
+    def set_compute(self, compute: str):
+        """Convolution operand precision: "fp32" (default, exact reference arithmetic) or
+        "bf16" (bf16 operands, fp32 accumulation; GroupNorm/softmax/attention stay fp32)."""
+        if compute not in ("fp32", "bf16"):
+            raise ValueError(f"compute must be 'fp32' or 'bf16', got {compute!r}")
+        self.compute = compute
+        return self
+
     def _signature(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
@@ -242,6 +251,7 @@ class UNetModel(nn.Module):
                            f"set_param {k}")
             _lib.check(lib.cfd_unet_ready(h), "cfd_unet_ready")
             entry[1] = sig
+        _lib.check(lib.cfd_unet_set_compute(entry[0], 1 if self.compute == "bf16" else 0), "cfd_unet_set_compute")
         return entry[0]
 
     def _workspace(self, h, device, B):
@@ -290,6 +300,8 @@ class UNetModel(nn.Module):
     def forward_tape(self, x: torch.Tensor, timesteps: torch.Tensor) -> torch.Tensor:
         """forward() that also records the activations for input_vjp (bit-identical eps)."""
         x, t, B = self._prep(x, timesteps)
+        if self.compute != "fp32":
+            raise NotImplementedError("the input-gradient (DPS) path is fp32: set_compute('fp32')")
         h = self._handle(x.device)
         lib = _lib.load()
         ws = self._workspace(h, x.device, B)

@@ -73,6 +73,16 @@ int  cfd_unet_ready(const cfd_unet* h);
 int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
 /* eps = UNetModel.forward(x, timesteps): x (B,1,H,W), t (B) int64 (already
  * remapped through timestep_map, respace.py:123-128), eps (B,1,H,W). */
+/* Convolution operand precision (config E, BASELINE.json configs[4]):
+ * CFD_COMPUTE_BF16 rounds both convolution operands to bf16 (RNE) and
+ * accumulates in fp32 on v_mfma_f32_16x16x32_bf16; GroupNorm, softmax,
+ * attention, the timestep MLP and the 1-channel in/out convolutions stay fp32.
+ * Default CFD_COMPUTE_F32 (exact fp32, the reference's arithmetic).  This
+ * replaces UNetModel's use_fp16 torso conversion (U/src/unet.py:619-633) with
+ * bf16 operands. */
+#define CFD_COMPUTE_F32  0
+#define CFD_COMPUTE_BF16 1
+int  cfd_unet_set_compute(cfd_unet* h, int compute);
 int  cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                       void* workspace, size_t ws_bytes, void* stream);
 

@@ -54,10 +54,10 @@ def bench_siren(latents=64, npts=64 ** 3, dims=(3, 64, 3, 15, 384), iters=3):
                       "tflops": flops / (best / 1e3) / 1e12}), flush=True)
 
 
-def bench_unet(batch=8, size=64, iters=10):
+def bench_unet(batch=8, size=64, iters=10, bf16=False):
     from confild_amd.script_util import create_model
     m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
-                     attention_resolutions="32,16,8")
+                     attention_resolutions="32,16,8", use_bf16=bf16)
     sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     m.to(DEV)
@@ -65,7 +65,8 @@ def bench_unet(batch=8, size=64, iters=10):
     t = torch.full((batch,), 500, dtype=torch.int64, device=DEV)
     med, best = timeit(lambda: m(x, t), iters=iters, warm=2)
     gf = {32: 19.23, 64: 68.61, 128: 140.75}.get(size, float("nan"))
-    print(json.dumps({"kernel": "unet_forward", "batch": batch, "size": size, "ms": med, "best_ms": best,
+    print(json.dumps({"kernel": "unet_forward", "compute": m.compute, "batch": batch, "size": size, "ms": med,
+                      "best_ms": best,
                       "tflops": batch * gf * 1e9 / (best / 1e3) / 1e12}), flush=True)
 
 
@@ -117,10 +118,11 @@ if __name__ == "__main__":
     ap.add_argument("--latents", type=int, default=64)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--bf16", action="store_true")
     a = ap.parse_args()
     if a.what in ("siren", "sweep"):
         bench_siren(a.latents)
     if a.what in ("unet", "sweep"):
-        bench_unet(a.batch, a.size)
+        bench_unet(a.batch, a.size, bf16=a.bf16)
     if a.what == "dps":
         bench_dps(a.batch, a.size)
