@@ -80,6 +80,8 @@ _SIGS = {
     "cfd_siren_set_param": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t]),
     "cfd_siren_ready": (C.c_int, [C.c_void_p]),
     "cfd_siren_workspace_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]),
+    "cfd_siren_set_compute": (C.c_int, [C.c_void_p, C.c_int]),
+    "cfd_siren_get_compute": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "cfd_siren_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                     C.c_size_t, C.c_void_p]),

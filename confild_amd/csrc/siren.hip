@@ -22,6 +22,8 @@
 //   * sin(w0*x) uses a Cody-Waite reduced polynomial (common.hpp sin_cw);
 //   * the last (H -> c) layer, the bias and the per-point de-normalisation are
 //     fused into the store.
+#include <cmath>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -29,54 +31,9 @@
 #include <utility>
 #include <vector>
 
-#include "common.hpp"
+#include "siren.hpp"
 
 namespace cfd {
-
-// Compile-time loop: f(std::integral_constant<int, I>) for I in [0, N).  Keeps
-// every register-array index static (a runtime index sends the array to scratch).
-template <int N, class F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
-}
-
-// coordinates per workgroup = 16 * waves (4 waves: 2 workgroups per CU; 8 waves:
-// one workgroup per CU, each LDS-DMA'd weight block shared by 128 coordinates)
-
-struct SirenArgs {
-    const float* w0;      // (H, d)            net1.0.weight
-    const float* wimg;    // nh * NB blocks of NB*256 floats (packed hidden weights)
-    const float* wout;    // (c, H)            net1.{nh+1}.weight
-    const float* bout;    // (c)               net1.{nh+1}.bias
-    const float* film;    // (b, nh+1, H)      b_i + V_i z
-    const float* coords;  // (N, d)
-    const float* xmax;
-    const float* xmin;
-    const float* ymax;
-    const float* ymin;
-    float* out;           // (b, N, c)
-    int64_t N;
-    int64_t ystride;
-    int64_t b0;           // first latent of this launch (grid.y chunking)
-    int d, c, nh;
-    float w0f;
-};
-
-template <int NB, int WAVES>
-__device__ __forceinline__ void siren_issue_block(const float* __restrict__ wimg, int J, float* dst,
-                                                  int wave, int lane) {
-    constexpr int BLK = NB * 256;
-    const float* src = wimg + (int64_t)J * BLK;
-    for (int piece = wave; piece < NB; piece += WAVES) {
-        __builtin_amdgcn_global_load_lds((const void*)(src + piece * 256 + lane * 4),
-                                         (__attribute__((address_space(3))) void*)(dst + piece * 256),
-                                         16, 0, 0);
-    }
-}
 
 // DUAL = false: one accumulation chain per 16-row block, 2 workgroups per CU
 //              (256 VGPRs: the partner workgroup hides the MFMA dependency);
@@ -520,6 +477,9 @@ struct cfd_siren {
     float* wout = nullptr;  // (c, H)
     float* bout = nullptr;  // (c)
     float* wimg_t = nullptr; // transposed weight image, layers nh..1 (latent-gradient path)
+    float* wimg16 = nullptr; // split-f16 image (hi, lo) of the scaled hidden weights, same bytes as wimg
+    float* wscale = nullptr; // (nh) power-of-two scale of each hidden layer in wimg16
+    int compute = CFD_SIREN_SPLIT_F16;
 };
 
 namespace {
@@ -575,6 +535,39 @@ void launch_siren(const cfd_siren* h, const cfd::SirenArgs& a, int b, hipStream_
 
 }  // namespace
 
+namespace {
+
+// Split-f16 image of hidden layer li (siren_split.hip): W s = Wh + Wl with
+// s = 2^-e, e = frexp exponent of max|W| (so max|W s| is in [0.5, 1)), both
+// halves RNE.  Block j, K-chunk q: 1 KiB of Wh then 1 KiB of Wl, lane-linear,
+// lane l element t = W[16j + l%16][16(2q + t/4) + 4(l/16) + t%4] (the A operand
+// of v_mfma_f32_16x16x32_f16 in the k order of the accumulator-as-B layout).
+void pack_split_f16(cfd_siren* h, int li, const float* W) {
+    const int H = h->cfg.hidden_features, NB = h->NB, NQ = NB / 2;
+    float amax = 0.f;
+    for (size_t i = 0; i < (size_t)H * H; ++i) amax = std::max(amax, std::fabs(W[i]));
+    int e = 0;
+    if (amax > 0.f) std::frexp(amax, &e);
+    const float s = std::ldexp(1.0f, -e);
+    std::vector<_Float16> img((size_t)NB * NB * 512);
+    for (int j = 0; j < NB; ++j)
+        for (int q = 0; q < NQ; ++q)
+            for (int l = 0; l < 64; ++l)
+                for (int t = 0; t < 8; ++t) {
+                    const float v = W[(size_t)(16 * j + l % 16) * H + 16 * (2 * q + t / 4) + 4 * (l / 16) + t % 4] * s;
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    const size_t base = ((size_t)j * NB + 2 * q) * 512 + l * 8 + t;
+                    img[base] = hi;
+                    img[base + 512] = lo;
+                }
+    CFD_HIP(hipMemcpy(h->wimg16 + (size_t)(li - 1) * NB * NB * 256, img.data(), img.size() * sizeof(_Float16),
+                      hipMemcpyHostToDevice));
+    CFD_HIP(hipMemcpy(h->wscale + (li - 1), &s, sizeof(float), hipMemcpyHostToDevice));
+}
+
+}  // namespace
+
 extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren** out) {
     return cfd::guard([&] {
         CFD_REQUIRE(cfg && out, CFD_EARG, "null argument");
@@ -607,6 +600,9 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_HIP(hipMalloc(&h->wout, sizeof(float) * c * H));
         CFD_HIP(hipMalloc(&h->bout, sizeof(float) * 4));
         CFD_HIP(hipMalloc(&h->wimg_t, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
+        CFD_HIP(hipMalloc(&h->wimg16, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
+        CFD_HIP(hipMalloc(&h->wscale, sizeof(float) * (size_t)std::max(nh, 1)));
+        if (const char* e = getenv("CFD_SIREN_COMPUTE")) h->compute = atoi(e);
         *out = h;
     });
 }
@@ -620,6 +616,8 @@ extern "C" void cfd_siren_destroy(cfd_siren* h) {
     (void)hipFree(h->wout);
     (void)hipFree(h->bout);
     (void)hipFree(h->wimg_t);
+    (void)hipFree(h->wimg16);
+    (void)hipFree(h->wscale);
     delete h;
 }
 
@@ -688,6 +686,7 @@ extern "C" int cfd_siren_set_param(cfd_siren* h, const char* key, const float* h
                                 host[(size_t)(16 * q + 4 * (lane >> 4) + s2) * H + 16 * j + (lane & 15)];
             CFD_HIP(hipMemcpy(h->wimg_t + (size_t)(nh - li) * NB * NB * 256, img.data(), img.size() * 4,
                               hipMemcpyHostToDevice));
+            if (NB % 2 == 0) pack_split_f16(h, li, host);
         }
         (void)c;
         prm->set = true;
@@ -743,7 +742,30 @@ extern "C" int cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, c
         a.c = h->cfg.out_features;
         a.nh = nh;
         a.w0f = h->cfg.w0;
-        launch_siren(h, a, b, st);
+        if (h->compute == CFD_SIREN_SPLIT_F16 && nh >= 1 && cfd::siren_split_supported(h->NB)) {
+            a.wimg = h->wimg16;
+            a.wscale = h->wscale;
+            cfd::launch_siren_split(h->NB, a, b, st);
+        } else {
+            launch_siren(h, a, b, st);
+        }
+    });
+}
+
+extern "C" int cfd_siren_set_compute(cfd_siren* h, int compute) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h, CFD_EARG, "null handle");
+        CFD_REQUIRE(compute == CFD_SIREN_F32 || compute == CFD_SIREN_SPLIT_F16, CFD_EARG, "unknown SIREN compute mode");
+        h->compute = compute;
+    });
+}
+
+extern "C" int cfd_siren_get_compute(const cfd_siren* h, int* compute) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && compute, CFD_EARG, "null argument");
+        const bool split = h->compute == CFD_SIREN_SPLIT_F16 && h->cfg.num_hidden_layers >= 1 &&
+                           cfd::siren_split_supported(h->NB);
+        *compute = split ? CFD_SIREN_SPLIT_F16 : CFD_SIREN_F32;
     });
 }
 

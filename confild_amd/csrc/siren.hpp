@@ -1,0 +1,62 @@
+// Shared pieces of the fused SIREN decoders (siren.hip: exact fp32 MFMA chain;
+// siren_split.hip: fp32-accurate split-f16 MFMA chain).
+#pragma once
+#include <type_traits>
+#include <utility>
+
+#include "common.hpp"
+
+namespace cfd {
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [0, N).  Keeps
+// every register-array index static (a runtime index sends the array to scratch).
+template <int N, class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+
+struct SirenArgs {
+    const float* w0;      // (H, d)            net1.0.weight
+    const float* wimg;    // nh * NB blocks of NB*256 floats (packed hidden weights)
+    const float* wout;    // (c, H)            net1.{nh+1}.weight
+    const float* bout;    // (c)               net1.{nh+1}.bias
+    const float* film;    // (b, nh+1, H)      b_i + V_i z
+    const float* coords;  // (N, d)
+    const float* xmax;
+    const float* xmin;
+    const float* ymax;
+    const float* ymin;
+    float* out;           // (b, N, c)
+    const float* wscale;  // (nh) power-of-two weight scale of each hidden layer (split-f16 image only)
+    int64_t N;
+    int64_t ystride;
+    int64_t b0;           // first latent of this launch (grid.y chunking)
+    int d, c, nh;
+    float w0f;
+};
+
+// LDS-DMA of one weight block (NB pieces of 1 KiB) into an LDS ring slot: one
+// global_load_lds_dwordx4 wave-instruction per piece, pieces spread over the waves.
+template <int NB, int WAVES>
+__device__ __forceinline__ void siren_issue_block(const float* __restrict__ wimg, int J, float* dst,
+                                                  int wave, int lane) {
+    constexpr int BLK = NB * 256;
+    // J through readfirstlane: keeps the block base a scalar (else the compiler
+    // precomputes one 64-bit VGPR address per unrolled block)
+    const float* src = wimg + (int64_t)__builtin_amdgcn_readfirstlane(J) * BLK;
+    for (int piece = wave; piece < NB; piece += WAVES) {
+        __builtin_amdgcn_global_load_lds((const void*)(src + piece * 256 + lane * 4),
+                                         (__attribute__((address_space(3))) void*)(dst + piece * 256),
+                                         16, 0, 0);
+    }
+}
+
+// Split-f16 chain (siren_split.hip).  Defined for even NB (H a multiple of 32).
+bool siren_split_supported(int NB);
+void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st);
+
+}  // namespace cfd

@@ -1,0 +1,307 @@
+// Fused SIREN/FiLM decoder on f16 MFMA with fp32-level accuracy (K7s).
+//
+// Same contract and per-(coordinate, latent) arithmetic as siren_fused
+// (siren.hip; reference N/cnf/nf_networks.py:480-495, components.py:19-25,64-76,
+// normalize.py:100-114), but every hidden-layer product W x runs as three
+// v_mfma_f32_16x16x32_f16 on a two-term f16 split of both operands:
+//     W s = Wh + Wl,  x = xh + xl   (xh = f16(x), xl = f16(x - xh), RNE)
+//     s W x ~= Wl xh + Wh xl + Wh xh          (fp32 accumulate; Wl xl dropped)
+// Each split carries 22 significant bits and the products are exact in fp32, so
+// the dot product's error is that of an fp32 accumulation (measured against an
+// fp64 evaluation: same max / mean error as the fp32 chain).
+// s = 2^-e per layer (host, from max|W|) keeps Wh/Wl in f16 normal range;
+// the accumulator starts at s F_i (FiLM) and the sine takes (w0/s) acc -- both
+// power-of-two rescalings, exact.  The f16 MFMA issues 16x the f32 MFMA rate,
+// so three of them cost 3/16 of the f32 chain.
+//
+// Layout: workgroup = WAVES x 16 coordinates, one latent (grid.y).  The B operand
+// of K-chunk q (32 features) is lane-local: lane (n, g) holds features
+// 16(2q + t/4) + 4g + t%4, t < 8, which are exactly the accumulator rows of
+// output blocks 2q and 2q+1 -- no shuffle between layers.  Hidden weights stream
+// through a 2-slot LDS ring by LDS-DMA, one 16-row block (NQ x {hi, lo} x 1 KiB)
+// per slot, read with ds_read_b128.  The sine + split of output block j runs
+// while block j+1's MFMAs issue (software pipelined, next-layer operands in a
+// second register set); the last hidden layer feeds the H -> c output layer in
+// fp32 directly.
+#include <cstdint>
+
+#include "siren.hpp"
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+
+namespace cfd {
+
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+// One MFMA operand (8 x f16) kept as 4 packed 32-bit words: writing a word is one
+// VGPR write (element inserts into an h8 value turn into v_perm chains).
+struct Frag {
+    unsigned w[4];
+    __device__ __forceinline__ h8 v() const { return __builtin_bit_cast(h8, (u4){w[0], w[1], w[2], w[3]}); }
+};
+
+// x (4 fp32) -> f16 hi/lo halves at positions [T, T+4) of (hi, lo): RNE both times
+template <int T>
+__device__ __forceinline__ void split4(const float (&x)[4], Frag& hi, Frag& lo) {
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+        const h2 h = __builtin_convertvector((f2){x[r], x[r + 1]}, h2);
+        const f2 hf = __builtin_convertvector(h, f2);
+        const h2 l = __builtin_convertvector((f2){x[r] - hf.x, x[r + 1] - hf.y}, h2);
+        hi.w[(T + r) / 2] = __builtin_bit_cast(unsigned, h);
+        lo.w[(T + r) / 2] = __builtin_bit_cast(unsigned, l);
+    }
+}
+
+// sin(x) for two lanes' values on packed fp32 math (v_pk_fma_f32 / v_pk_mul_f32
+// do two elements per issue).  Same reduction constants and polynomial as
+// sin_cw (common.hpp); the quotient q = rint(x / pi) comes from the 1.5*2^23
+// round-to-integer constant (exact for |x| < 2^21 pi), whose low mantissa bit is
+// the parity that sets the sign.  The reduction is exact for |x| < 39000 (as
+// sin_cw) and degrades gradually beyond (no v_sin_f32 fallback: its valid
+// domain ends at 256 revolutions = 1608); q is right for |x| < 2^21 pi.
+__device__ __forceinline__ f2 sin2_cw(f2 x) {
+    const f2 magic = {12582912.0f, 12582912.0f};
+    const f2 t = __builtin_elementwise_fma(x, (f2){0.318309886183790671538f, 0.318309886183790671538f}, magic);
+    const f2 q = t - magic;
+    f2 r = __builtin_elementwise_fma(q, (f2){-3.140625f, -3.140625f}, x);
+    r = __builtin_elementwise_fma(q, (f2){-0.0009670257568359375f, -0.0009670257568359375f}, r);
+    r = __builtin_elementwise_fma(q, (f2){-6.2771141529083251953e-07f, -6.2771141529083251953e-07f}, r);
+    r = __builtin_elementwise_fma(q, (f2){-1.2154201256553420762e-10f, -1.2154201256553420762e-10f}, r);
+    const f2 s = r * r;
+    f2 u = (f2){2.6083159809786593541503e-06f, 2.6083159809786593541503e-06f};
+    u = __builtin_elementwise_fma(u, s, (f2){-0.0001981069071916863322258f, -0.0001981069071916863322258f});
+    u = __builtin_elementwise_fma(u, s, (f2){0.00833307858556509017944336f, 0.00833307858556509017944336f});
+    u = __builtin_elementwise_fma(u, s, (f2){-0.166666597127914428710938f, -0.166666597127914428710938f});
+    const f2 y = __builtin_elementwise_fma(s, u * r, r);
+    // (element-wise scalar bit casts here were miscompiled into a lane copy)
+    const u2 sg = __builtin_bit_cast(u2, t) << 31;
+    return __builtin_bit_cast(f2, __builtin_bit_cast(u2, y) ^ sg);
+}
+
+template <int NB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 2) void siren_fused_split(SirenArgs p) {
+    static_assert(NB % 2 == 0, "split-f16 chain needs H % 32 == 0");
+    constexpr int NQ = NB / 2;
+    constexpr int TILE = 16 * WAVES;
+    constexpr int H = NB * 16;
+    constexpr int BLK = NB * 256;  // floats per block slot: NQ x (hi, lo) x 512 halves
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int nh = p.nh;
+    float* wbuf = smem;                  // 2 slots
+    float* film = smem + 2 * BLK;        // (nh+1) x H
+    float* w0s = film + (nh + 1) * H;    // (H, 4)
+    float* wos = w0s + 4 * H;            // (4, H) output weights
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int g = lane >> 4;
+    const int j16 = lane & 15;
+    const int64_t b = p.b0 + blockIdx.y;
+    const int64_t n = (int64_t)blockIdx.x * TILE + wave * 16 + j16;
+    const int64_t nc = n < p.N ? n : p.N - 1;
+
+    {
+        const float* fsrc = p.film + b * (int64_t)(nh + 1) * H;
+        const int nf = (nh + 1) * H;
+        for (int i = threadIdx.x * 4; i < nf; i += 64 * WAVES * 4) *(f4*)(film + i) = *(const f4*)(fsrc + i);
+    }
+    for (int f = threadIdx.x; f < H; f += 64 * WAVES) {
+        f4 w = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < p.d; ++k) w[k] = p.w0[f * p.d + k];
+        *(f4*)(w0s + 4 * f) = w;
+    }
+    for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) wos[i] = i < p.c * H ? p.wout[i] : 0.f;
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < p.d) {
+            float v = p.coords[nc * p.d + k];
+            if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+            cn[k] = v;
+        }
+    }
+
+    __syncthreads();
+    siren_issue_block<NB, WAVES>(p.wimg, 0, wbuf, wave, lane);  // nh >= 1 (host-checked)
+
+    Frag BH[NQ], BL[NQ], NH[NQ], NL[NQ];
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    // output layer partial sums over this lane's 4 features of block j
+    auto out_acc = [&](int j, const float (&x)[4]) {
+#pragma unroll
+        for (int oc = 0; oc < 4; ++oc) {
+            if (oc < p.c) {
+                const f4 w = *(const f4*)(wos + oc * H + 16 * j + 4 * g);
+                o[oc] = fmaf(w.x, x[0], o[oc]);
+                o[oc] = fmaf(w.y, x[1], o[oc]);
+                o[oc] = fmaf(w.z, x[2], o[oc]);
+                o[oc] = fmaf(w.w, x[3], o[oc]);
+            }
+        }
+    };
+
+    // ---- layer 0 (d -> H, fp32 VALU): x = sin(w0 (W0 c + F_0)) ----
+    static_for<NB>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
+        float u[4], x[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
+            float a = cn[0] * w[0];
+#pragma unroll
+            for (int k = 1; k < 4; ++k)
+                if (k < p.d) a = fmaf(cn[k], w[k], a);
+            u[r] = p.w0f * (a + fv[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+            const f2 v = sin2_cw((f2){u[r], u[r + 1]});
+            x[r] = v.x;
+            x[r + 1] = v.y;
+        }
+        split4<4 * (q & 1)>(x, BH[q / 2], BL[q / 2]);
+    });
+
+    // ---- hidden layers: 3 f16 MFMAs per fp32 product ----
+    const int nblocks = nh * NB;
+    int J = 0;
+    for (int layer = 1; layer <= nh; ++layer) {
+        const bool last = layer == nh;
+        const float s = p.wscale[layer - 1];
+        const float m = p.w0f / s;  // power-of-two scale: exact
+        // sine + split (or output-layer accumulation) of output block j, in two
+        // halves that land between the MFMAs of the first K-chunks of block j+1
+        float x[4];
+        auto sine = [&](int h, const f4& a) __attribute__((always_inline)) {
+            const f2 v = sin2_cw((f2){a[2 * h], a[2 * h + 1]} * m);
+            x[2 * h] = v.x;
+            x[2 * h + 1] = v.y;
+            // pin the sine to this K-chunk (IR passes would otherwise sink every
+            // block's epilogue to the layer end, keeping NB accumulators live)
+            asm volatile("" : "+v"(x[2 * h]), "+v"(x[2 * h + 1]));
+        };
+        auto finish = [&](auto jc) __attribute__((always_inline)) {
+            constexpr int j = decltype(jc)::value;
+            if (last)
+                out_acc(j, x);
+            else {
+                split4<4 * (j & 1)>(x, NH[j / 2], NL[j / 2]);
+                constexpr int w = 2 * (j & 1);
+                asm volatile("" : "+v"(NH[j / 2].w[w]), "+v"(NH[j / 2].w[w + 1]), "+v"(NL[j / 2].w[w]),
+                             "+v"(NL[j / 2].w[w + 1]));
+            }
+        };
+        constexpr int QS1 = NQ > 1 ? 1 : 0, QFIN = NQ > 2 ? 2 : NQ - 1;
+        f4 prev;
+        static_for<NB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (J + 1 < nblocks) siren_issue_block<NB, WAVES>(p.wimg, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            const float* wb = wbuf + (J & 1) * BLK;
+            f4 a = *(const f4*)(film + layer * H + 16 * j + 4 * g) * s;
+            h8 ah = *(const h8*)(wb + lane * 4);
+            h8 al = *(const h8*)(wb + 256 + lane * 4);
+            static_for<NQ>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                h8 nah, nal;
+                if constexpr (q + 1 < NQ) {
+                    nah = *(const h8*)(wb + (q + 1) * 512 + lane * 4);
+                    nal = *(const h8*)(wb + (q + 1) * 512 + 256 + lane * 4);
+                }
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, BH[q].v(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BL[q].v(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BH[q].v(), a, 0, 0, 0);
+                if constexpr (j > 0) {
+                    if constexpr (q == 0) sine(0, prev);
+                    if constexpr (q == QS1) sine(1, prev);
+                    if constexpr (q == QFIN) finish(std::integral_constant<int, j - 1>{});
+                }
+                if constexpr (q + 1 < NQ) {
+                    ah = nah;
+                    al = nal;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            prev = a;
+            // block J+1 landed (this wave's pieces); the barrier publishes every
+            // wave's pieces and retires all reads of slot J&1 before its refill
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            ++J;
+        });
+        sine(0, prev);
+        sine(1, prev);
+        finish(std::integral_constant<int, NB - 1>{});
+        static_for<NQ>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            BH[q] = NH[q];
+            BL[q] = NL[q];
+        });
+    }
+
+    // ---- output layer (H -> c): reduce the 4 lane groups, bias, de-normalise ----
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        float s = o[oc];
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        o[oc] = oc < p.c ? s + p.bout[oc] : 0.f;
+    }
+    if (n < p.N && g < p.c) {
+        float v = g == 0 ? o[0] : g == 1 ? o[1] : g == 2 ? o[2] : o[3];
+        if (p.ymax) {
+            const int64_t yi = n * p.ystride + g;
+            const float hi = p.ymax[yi], lo = p.ymin[yi];
+            v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
+        }
+        p.out[(b * p.N + n) * p.c + g] = v;
+    }
+}
+
+namespace {
+constexpr int kSplitWaves = 8;
+
+template <int NB>
+void launch_nb(SirenArgs a, int b, hipStream_t st) {
+    constexpr int H = NB * 16;
+    const size_t lds = sizeof(float) * ((size_t)2 * NB * 256 + (size_t)(a.nh + 1) * H + 8 * H);
+    const void* fn = (const void*)siren_fused_split<NB, kSplitWaves>;
+    CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the split-f16 decoder's LDS staging");
+    CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int64_t tiles = ceil_div(a.N, 16 * kSplitWaves);
+    CFD_REQUIRE(tiles <= 0x7fffffff, CFD_EARG, "too many coordinates for one launch");
+    for (int64_t b0 = 0; b0 < b; b0 += 65535) {
+        a.b0 = b0;
+        const int nb = (int)std::min<int64_t>(65535, b - b0);
+        hipLaunchKernelGGL((siren_fused_split<NB, kSplitWaves>), dim3((unsigned)tiles, nb), dim3(64 * kSplitWaves),
+                           lds, st, a);
+        check_launch("siren_fused_split");
+    }
+}
+}  // namespace
+
+bool siren_split_supported(int NB) {
+    switch (NB) {
+        case 2: case 4: case 6: case 8: case 12: case 16: case 24: return true;
+        default: return false;
+    }
+}
+
+void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st) {
+    switch (NB) {
+        case 2: return launch_nb<2>(a, b, st);
+        case 4: return launch_nb<4>(a, b, st);
+        case 6: return launch_nb<6>(a, b, st);
+        case 8: return launch_nb<8>(a, b, st);
+        case 12: return launch_nb<12>(a, b, st);
+        case 16: return launch_nb<16>(a, b, st);
+        case 24: return launch_nb<24>(a, b, st);
+        default: throw Error{CFD_EARG, "split-f16 SIREN needs hidden_features = 32*{1,2,3,4,6,8,12,16}"};
+    }
+}
+
+}  // namespace cfd

@@ -69,6 +69,24 @@ class SIRENAutodecoder_film(nn.Module):
         if bias_init is not None:
             self.net2.apply(bias_init)
         self._handles = {}
+        self._compute = None  # None: the library default (CFD_SIREN_SPLIT_F16 where H % 32 == 0)
+
+    COMPUTE_MODES = {"f32": 0, "split_f16": 1}
+
+    def set_compute(self, mode: str):
+        """Hidden-layer arithmetic of the fused decoder: "split_f16" (3 f16 MFMAs on
+        two-term splits, fp32-level error; the default) or "f32" (exact fp32 MFMA)."""
+        if mode not in self.COMPUTE_MODES:
+            raise ValueError(f"compute mode {mode!r} not in {sorted(self.COMPUTE_MODES)}")
+        self._compute = mode
+        return self
+
+    def compute_mode(self, device) -> str:
+        """The mode a decode on `device` actually runs (split_f16 falls back to f32
+        when H % 32 != 0 or there is no hidden layer)."""
+        v = C.c_int()
+        _lib.check(_lib.load().cfd_siren_get_compute(self._handle(device), C.byref(v)), "cfd_siren_get_compute")
+        return {v_: k for k, v_ in self.COMPUTE_MODES.items()}[v.value]
 
     # -- device handle --------------------------------------------------------
     def _signature(self):
@@ -93,6 +111,8 @@ class SIRENAutodecoder_film(nn.Module):
                            f"siren set_param {k}")
             _lib.check(lib.cfd_siren_ready(entry[0]), "cfd_siren_ready")
             entry[1] = sig
+        if self._compute is not None:
+            _lib.check(lib.cfd_siren_set_compute(entry[0], self.COMPUTE_MODES[self._compute]), "cfd_siren_set_compute")
         return entry[0]
 
     # -- forward ----------------------------------------------------------------

@@ -179,6 +179,19 @@ int  cfd_siren_workspace_bytes(const cfd_siren* h, int b, size_t* bytes);
  *   ymax/ymin: output normaliser params with row stride y_stride (elements) per
  *              coordinate: y_stride = c for a per-point (N, c) table (lumped
  *              latent, train.py:194-201), 0 for a (c) table; NULL = raw output. */
+/* Hidden-layer arithmetic of cfd_siren_forward:
+ * CFD_SIREN_SPLIT_F16 (default; H a multiple of 32, nh >= 1): every product W x
+ *   as three v_mfma_f32_16x16x32_f16 on two-term f16 splits of the power-of-two
+ *   scaled weights and of the activations (Wl xh + Wh xl + Wh xh, fp32
+ *   accumulate): 22-bit operands, exact products, fp32 accumulation -- the error
+ *   against an fp64 evaluation matches the fp32 chain's;
+ * CFD_SIREN_F32: the exact fp32 v_mfma_f32_16x16x4_f32 chain.
+ * Env CFD_SIREN_COMPUTE overrides the default at handle creation.
+ * cfd_siren_get_compute reports the mode a forward actually runs. */
+#define CFD_SIREN_F32       0
+#define CFD_SIREN_SPLIT_F16 1
+int  cfd_siren_set_compute(cfd_siren* h, int compute);
+int  cfd_siren_get_compute(const cfd_siren* h, int* compute);
 int  cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, const float* latents, int b,
                        const float* xmax, const float* xmin,
                        const float* ymax, const float* ymin, int64_t y_stride,

@@ -1,0 +1,102 @@
+"""Split-f16 SIREN decoder (K7s, confild_amd/csrc/siren_split.hip) against an
+fp64 evaluation of the reference forward (N/cnf/nf_networks.py:480-495) and
+against the exact fp32 MFMA chain.
+
+The claim under test: the split-f16 chain is an fp32-accuracy decoder, i.e. its
+error against fp64 is that of an fp32 evaluation (bounded by 2x the fp32
+chain's error plus 1e-7 of the output scale), and it meets the same 2e-5
+tolerance against the fp32 oracle as every other SIREN test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from confild_amd import synth
+from confild_amd.nf_networks import SIRENAutodecoder_film
+from confild_amd.normalize import Normalizer_ts
+from oracle import siren as osn
+
+DEV = torch.device("cuda", 0)
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(dims, N, b, seed=1234):
+    d, L, c, nh, H = dims
+    sd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(seed, d, L, c, nh, H).items()}
+    net = SIRENAutodecoder_film(d, L, c, nh, H)
+    net.load_state_dict(sd)
+    net.to(DEV)
+    coords = torch.from_numpy(synth.uniform(7, "co", (N, d), 0.0, 1.0))
+    lat = torch.from_numpy(synth.normal(11, "la", (b, L))) * 0.5
+    ymax = torch.from_numpy(synth.uniform(9, "yx", (1, N, c), 0.5, 2.0))
+    ymin = -torch.from_numpy(synth.uniform(9, "yn", (1, N, c), 0.5, 2.0))
+    return sd, net, coords, lat, ymax, ymin
+
+
+def _decode(net, mode, coords, lat, ymax, ymin):
+    d = coords.shape[1]
+    net.set_compute(mode)
+    xn = Normalizer_ts(params=(torch.ones(1, d), torch.zeros(1, d)), method="-11", dim=0)
+    yn = Normalizer_ts(params=(ymax, ymin), method="-11", dim=0)
+    out = net.decode(coords.to(DEV), lat.to(DEV)[:, None], xn, yn).cpu().double()
+    return out, net.compute_mode(DEV)
+
+
+@pytest.mark.parametrize("dims,N,b", [((3, 64, 3, 15, 384), 4099, 3), ((3, 384, 3, 15, 384), 1000, 2),
+                                      ((2, 128, 2, 17, 256), 777, 4), ((2, 32, 3, 10, 128), 1000, 2),
+                                      ((3, 16, 1, 2, 64), 333, 5), ((2, 8, 4, 1, 32), 129, 3)])
+def test_split_f16_has_fp32_accuracy(hip, dims, N, b):
+    d, L, c, nh, H = dims
+    sd, net, coords, lat, ymax, ymin = _setup(dims, N, b)
+    sd64 = {k: v.double() for k, v in sd.items()}
+    ref64 = osn.decode(sd64, coords.double(), lat.double(), torch.ones(1, d, dtype=torch.float64),
+                       torch.zeros(1, d, dtype=torch.float64), ymax.double(), ymin.double())
+    ref32 = osn.decode(sd, coords, lat, torch.ones(1, d), torch.zeros(1, d), ymax, ymin).double()
+    split, mode_s = _decode(net, "split_f16", coords, lat, ymax, ymin)
+    f32, mode_f = _decode(net, "f32", coords, lat, ymax, ymin)
+    assert (mode_s, mode_f) == ("split_f16", "f32")
+    scale = ref64.abs().max().item()
+    e_split = (split - ref64).abs()
+    e_f32 = (f32 - ref64).abs()
+    e_cpu = (ref32 - ref64).abs()
+    print(f"{dims}: max err vs fp64 split {e_split.max():.3e} f32-MFMA {e_f32.max():.3e} cpu-fp32 {e_cpu.max():.3e}; "
+          f"mean split {e_split.mean():.3e} f32 {e_f32.mean():.3e}")
+    assert e_split.max().item() <= 2 * max(e_f32.max().item(), e_cpu.max().item()) + 1e-7 * scale
+    assert e_split.mean().item() <= 2 * max(e_f32.mean().item(), e_cpu.mean().item()) + 1e-8 * scale
+    assert (split - ref32).abs().max().item() <= 2e-5 * max(1.0, ref32.abs().max().item())
+
+
+def test_split_f16_falls_back_where_undefined(hip):
+    # H = 48 (odd number of 16-row blocks): the split chain needs H % 32 == 0
+    dims = (2, 8, 2, 3, 48)
+    sd, net, coords, lat, ymax, ymin = _setup(dims, 100, 2)
+    out, mode = _decode(net, "split_f16", coords, lat, ymax, ymin)
+    assert mode == "f32"
+    ref = osn.decode(sd, coords, lat, torch.ones(1, 2), torch.zeros(1, 2), ymax, ymin).double()
+    assert (out - ref).abs().max().item() <= 2e-5 * max(1.0, ref.abs().max().item())
+
+
+def test_split_f16_large_weights_scale(hip):
+    # weights 100x the SIREN init: the per-layer power-of-two scale keeps Wh/Wl in
+    # f16 range; w0 is lowered so the pre-activations stay in sin's exact range
+    dims = (3, 16, 3, 4, 128)
+    sd, net, coords, lat, ymax, ymin = _setup(dims, 500, 2, seed=99)
+    with torch.no_grad():
+        for i in range(1, 5):
+            net.net1[i].weight.mul_(100.0)
+    net.w0 = 0.3
+    net._handles = {}
+    sd2 = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    osn_w0 = osn.W0
+    try:
+        osn.W0 = 0.3
+        ref64 = osn.decode({k: v.double() for k, v in sd2.items()}, coords.double(), lat.double(),
+                           torch.ones(1, 3, dtype=torch.float64), torch.zeros(1, 3, dtype=torch.float64),
+                           ymax.double(), ymin.double())
+    finally:
+        osn.W0 = osn_w0
+    split, _ = _decode(net, "split_f16", coords, lat, ymax, ymin)
+    f32, _ = _decode(net, "f32", coords, lat, ymax, ymin)
+    e_s, e_f = (split - ref64).abs().max().item(), (f32 - ref64).abs().max().item()
+    assert e_s <= 2 * e_f + 1e-7 * ref64.abs().max().item()

@@ -39,17 +39,20 @@ def timeit(fn, iters=5, warm=1):
     return ts[len(ts) // 2], ts[0]
 
 
-def bench_siren(latents=64, npts=64 ** 3, dims=(3, 64, 3, 15, 384), iters=3):
+def bench_siren(latents=64, npts=64 ** 3, dims=(3, 64, 3, 15, 384), iters=3, compute=None):
     from confild_amd.nf_networks import SIRENAutodecoder_film
     d, L, c, nh, H = dims
     net = SIRENAutodecoder_film(d, L, c, nh, H)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, d, L, c, nh, H).items()})
     net.to(DEV)
+    if compute:
+        net.set_compute(compute)
     coords = torch.rand(npts, d, device=DEV)
     lat = torch.randn(latents, 1, L, device=DEV) * 0.5
     med, best = timeit(lambda: net(coords, lat), iters=iters)
     flops = latents * npts * 2 * (d * H + nh * H * H + H * c)
-    print(json.dumps({"kernel": "siren", "variant": os.environ.get("CFD_SIREN_VARIANT", "0"), "dims": dims,
+    print(json.dumps({"kernel": "siren", "compute": net.compute_mode(DEV),
+                      "variant": os.environ.get("CFD_SIREN_VARIANT", "0"), "dims": dims,
                       "latents": latents, "npts": npts, "ms": med, "best_ms": best,
                       "tflops": flops / (best / 1e3) / 1e12}), flush=True)
 
@@ -119,9 +122,11 @@ if __name__ == "__main__":
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--compute", choices=["f32", "split_f16"], default=None)
+    ap.add_argument("--dims", default="3,64,3,15,384", help="SIREN d,L,c,nh,H")
     a = ap.parse_args()
     if a.what in ("siren", "sweep"):
-        bench_siren(a.latents)
+        bench_siren(a.latents, dims=tuple(int(v) for v in a.dims.split(",")), compute=a.compute)
     if a.what in ("unet", "sweep"):
         bench_unet(a.batch, a.size, bf16=a.bf16)
     if a.what == "dps":
