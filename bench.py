@@ -13,8 +13,14 @@ network access for checkpoints.  Multi-GPU: one process per GPU (torchrun), each
 rank generates its own batch of 8 (weak scaling, no data-path collective).
 
 Prints ONE JSON line (rank 0) with the driver contract plus a ``roofline`` object
-for the dominant kernel (siren_fused, timed with HIP events on its stream) and a
-``cpu_baseline`` measured on this host's cores with the oracle (rank 0, N=1).
+for the dominant kernel (the CNF decoder, timed with HIP events on its stream) and
+a ``cpu_baseline`` measured on this host's cores with the oracle (rank 0, N=1).
+
+The decoder's hidden layers run by default as split-f16 (siren_fused_split: three
+f16 MFMAs per fp32 product on 22-bit operand splits, fp32-level error against an
+fp64 evaluation -- tests/test_gpu_siren_split.py); its roofline is the f16 dense
+MFMA peak / 3.  ``--siren-compute f32`` runs the exact fp32 MFMA chain
+(siren_fused) against the fp32 MFMA peak instead.
 """
 from __future__ import annotations
 
@@ -35,23 +41,30 @@ S = 64           # latent image (T = L = 64)
 STEPS = "256"    # timestep respacing
 GRID = 64        # 64^3 lattice
 CNF = dict(d=3, L=64, c=3, nh=15, H=384)
-FMA_PEAK_TFLOPS = 157.3   # MI355X fp32 matrix peak (MI355X_MICROARCH.md chip table)
+FMA_PEAK_TFLOPS = 157.3    # MI355X fp32 matrix peak (MI355X_MICROARCH.md chip table)
+F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16/bf16 matrix peak (same table; no sparsity)
 HBM_PEAK_GBS = 8000.0
 
+# dominant-kernel roofline per decoder compute mode:
+#   (kernel name, peak in algorithmic fp32 TFLOP/s, basis, committed PMC record)
+ROOFLINE = {
+    "split_f16": ("siren_fused_split", F16_PEAK_TFLOPS / 3,
+                  "f16 dense MFMA peak / 3 (three f16 MFMAs per fp32 product)", "r01_siren_split_pmc.json"),
+    "f32": ("siren_fused", FMA_PEAK_TFLOPS, "fp32 MFMA peak", "r01_siren_pmc.json"),
+}
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_siren_pmc.json")
 
-
-def measured_traffic(latents, npts):
-    """Per-launch fabric bytes of siren_fused from the committed rocprofv3 PMC
-    record (tools/pmc_traffic.py), scaled from its launch geometry to this one."""
+def measured_traffic(mode, latents, npts):
+    """Per-launch fabric bytes of the decoder kernel from the committed rocprofv3
+    PMC record (tools/pmc_traffic.py), scaled from its launch geometry to this one."""
+    kname, _, _, fname = ROOFLINE[mode]
     try:
-        rec = json.load(open(PMC_FILE))
+        rec = json.load(open(os.path.join(ROOT, "profiles", fname)))
     except (OSError, ValueError):
         return None
     launch = rec.get("launch", {})
     ref_pairs = launch.get("latents", 0) * launch.get("coords", 0)
-    if not ref_pairs or "siren_fused" not in rec.get("kernel", ""):
+    if not ref_pairs or f"{kname}<" not in rec.get("kernel", ""):
         return None
     return rec["traffic_bytes_per_launch"] * (latents * npts) / ref_pairs
 
@@ -65,7 +78,7 @@ def unet_flops_per_sample():
     return 68.61e9
 
 
-def setup(dev):
+def setup(dev, siren_compute="split_f16"):
     from confild_amd import synth
     from confild_amd.nf_networks import SIRENAutodecoder_film
     from confild_amd.normalize import Normalizer_ts
@@ -81,6 +94,7 @@ def setup(dev):
     nf.load_state_dict({k: torch.from_numpy(v) for k, v in
                         synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"], c["H"]).items()})
     nf.to(dev)
+    nf.set_compute(siren_compute)
     ax = torch.linspace(0, 1, GRID)
     coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3).to(dev)
     N = coords.shape[0]
@@ -166,6 +180,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--siren-compute", choices=["split_f16", "f32"], default="split_f16")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,7 +193,9 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    objs = setup(dev)
+    objs = setup(dev, args.siren_compute)
+    mode = objs[2].compute_mode(dev)
+    kname, peak, peak_basis, _ = ROOFLINE[mode]
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -221,12 +238,16 @@ def main():
             "value": value, "unit": "fields/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded weights and inputs; no checkpoints)",
+            "compute": {"unet": "fp32 (v_mfma_f32_16x16x4_f32)",
+                        "cnf_decoder": ("fp32 via split-f16 (3x v_mfma_f32_16x16x32_f16 on 22-bit operand "
+                                        "splits; error vs fp64 = fp32's, DESIGN.md K7s)" if mode == "split_f16"
+                                        else "fp32 (v_mfma_f32_16x16x4_f32)")},
             "config": {"workload": "Case4 uncond: U-Net 64x64 B=8/GPU, DDPM 256 steps (cosine, respaced), "
                                    "CNF SIREN(3,64,3,15,384) decode of 8x64 latents on a 64^3 lattice",
                        "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world} (independent batches)"},
-            "roofline": {"bound": "mfma", "kernel": "siren_fused (+siren_film)", "achieved": achieved,
-                         "peak": FMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FMA_PEAK_TFLOPS,
-                         "traffic": measured_traffic(B * S, GRID ** 3), "flops_per_launch": flops,
+            "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)", "achieved": achieved,
+                         "peak": peak, "peak_basis": peak_basis, "unit": "TFLOP/s", "frac": achieved / peak,
+                         "traffic": measured_traffic(mode, B * S, GRID ** 3), "flops_per_launch": flops,
                          "launch_ms": dec_s * 1e3,
                          "unet_share_ms": (elapsed / args.steps - dec_s) * 1e3},
             "cpu_baseline": cpu,

@@ -24,6 +24,8 @@
 // second register set); the last hidden layer feeds the H -> c output layer in
 // fp32 directly.
 #include <cstdint>
+#include <cstdlib>
+#include <algorithm>
 
 #include "siren.hpp"
 
@@ -78,21 +80,27 @@ __device__ __forceinline__ f2 sin2_cw(f2 x) {
     u = __builtin_elementwise_fma(u, s, (f2){-0.166666597127914428710938f, -0.166666597127914428710938f});
     const f2 y = __builtin_elementwise_fma(s, u * r, r);
     // (element-wise scalar bit casts here were miscompiled into a lane copy)
+    // adding t << 31 to the bits of y flips exactly the sign bit: one v_lshl_add_u32
     const u2 sg = __builtin_bit_cast(u2, t) << 31;
-    return __builtin_bit_cast(f2, __builtin_bit_cast(u2, y) ^ sg);
+    return __builtin_bit_cast(f2, __builtin_bit_cast(u2, y) + sg);
 }
 
-template <int NB, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, 2) void siren_fused_split(SirenArgs p) {
+// s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
+constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
+
+// CG column groups of 16 coordinates per wave share every A-fragment read (CG = 2:
+// one wave per SIMD, 512 registers; CG = 1: two waves per SIMD, 256 registers).
+template <int NB, int WAVES, int RING, int CG, bool NOSYNC = false>
+__global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split(SirenArgs p) {
     static_assert(NB % 2 == 0, "split-f16 chain needs H % 32 == 0");
     constexpr int NQ = NB / 2;
-    constexpr int TILE = 16 * WAVES;
+    constexpr int TILE = 16 * CG * WAVES;
     constexpr int H = NB * 16;
     constexpr int BLK = NB * 256;  // floats per block slot: NQ x (hi, lo) x 512 halves
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int nh = p.nh;
-    float* wbuf = smem;                  // 2 slots
-    float* film = smem + 2 * BLK;        // (nh+1) x H
+    float* wbuf = smem;                  // RING slots
+    float* film = smem + RING * BLK;     // (nh+1) x H
     float* w0s = film + (nh + 1) * H;    // (H, 4)
     float* wos = w0s + 4 * H;            // (4, H) output weights
 
@@ -101,8 +109,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void siren_fused_split(SirenArgs p) 
     const int g = lane >> 4;
     const int j16 = lane & 15;
     const int64_t b = p.b0 + blockIdx.y;
-    const int64_t n = (int64_t)blockIdx.x * TILE + wave * 16 + j16;
-    const int64_t nc = n < p.N ? n : p.N - 1;
+    const int64_t n0 = (int64_t)blockIdx.x * TILE + wave * 16 * CG + j16;  // + 16 c
 
     {
         const float* fsrc = p.film + b * (int64_t)(nh + 1) * H;
@@ -115,31 +122,46 @@ __global__ __launch_bounds__(64 * WAVES, 2) void siren_fused_split(SirenArgs p) 
         *(f4*)(w0s + 4 * f) = w;
     }
     for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) wos[i] = i < p.c * H ? p.wout[i] : 0.f;
-    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+    float cn[CG][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (k < p.d) {
-            float v = p.coords[nc * p.d + k];
-            if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
-            cn[k] = v;
+    for (int c = 0; c < CG; ++c) {
+        const int64_t n = n0 + 16 * c;
+        const int64_t nc = n < p.N ? n : p.N - 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float v = 0.f;
+            if (k < p.d) {
+                v = p.coords[nc * p.d + k];
+                if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+            }
+            cn[c][k] = v;
         }
     }
 
     __syncthreads();
-    siren_issue_block<NB, WAVES>(p.wimg, 0, wbuf, wave, lane);  // nh >= 1 (host-checked)
+    const int nblocks = nh * NB;  // nh >= 1 (host-checked)
+    for (int k = 0; k < RING - 1; ++k)
+        if (k < nblocks) siren_issue_block<NB, WAVES>(p.wimg, k, wbuf + k * BLK, wave, lane);
+    // LDS-DMA pieces this wave issues per block (the in-flight count its vmcnt waits see)
+    constexpr int PC_LO = NB / WAVES, PC_HI = (NB + WAVES - 1) / WAVES;
+    const bool pc_hi = wave < NB % WAVES;
 
-    Frag BH[NQ], BL[NQ], NH[NQ], NL[NQ];
-    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    Frag BH[CG][NQ], BL[CG][NQ], NH[CG][NQ], NL[CG][NQ];
+    float o[CG][4];
+#pragma unroll
+    for (int c = 0; c < CG; ++c)
+#pragma unroll
+        for (int oc = 0; oc < 4; ++oc) o[c][oc] = 0.f;
     // output layer partial sums over this lane's 4 features of block j
-    auto out_acc = [&](int j, const float (&x)[4]) {
+    auto out_acc = [&](int c, int j, const float (&x)[4]) __attribute__((always_inline)) {
 #pragma unroll
         for (int oc = 0; oc < 4; ++oc) {
             if (oc < p.c) {
                 const f4 w = *(const f4*)(wos + oc * H + 16 * j + 4 * g);
-                o[oc] = fmaf(w.x, x[0], o[oc]);
-                o[oc] = fmaf(w.y, x[1], o[oc]);
-                o[oc] = fmaf(w.z, x[2], o[oc]);
-                o[oc] = fmaf(w.w, x[3], o[oc]);
+                o[c][oc] = fmaf(w.x, x[0], o[c][oc]);
+                o[c][oc] = fmaf(w.y, x[1], o[c][oc]);
+                o[c][oc] = fmaf(w.z, x[2], o[c][oc]);
+                o[c][oc] = fmaf(w.w, x[3], o[c][oc]);
             }
         }
     };
@@ -148,61 +170,73 @@ __global__ __launch_bounds__(64 * WAVES, 2) void siren_fused_split(SirenArgs p) 
     static_for<NB>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
         const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
-        float u[4], x[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
-            float a = cn[0] * w[0];
+        for (int c = 0; c < CG; ++c) {
+            float u[4], x[4];
 #pragma unroll
-            for (int k = 1; k < 4; ++k)
-                if (k < p.d) a = fmaf(cn[k], w[k], a);
-            u[r] = p.w0f * (a + fv[r]);
+            for (int r = 0; r < 4; ++r) {
+                const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
+                float a = cn[c][0] * w[0];
+#pragma unroll
+                for (int k = 1; k < 4; ++k)
+                    if (k < p.d) a = fmaf(cn[c][k], w[k], a);
+                u[r] = p.w0f * (a + fv[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+                const f2 v = sin2_cw((f2){u[r], u[r + 1]});
+                x[r] = v.x;
+                x[r + 1] = v.y;
+            }
+            split4<4 * (q & 1)>(x, BH[c][q / 2], BL[c][q / 2]);
         }
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-            const f2 v = sin2_cw((f2){u[r], u[r + 1]});
-            x[r] = v.x;
-            x[r + 1] = v.y;
-        }
-        split4<4 * (q & 1)>(x, BH[q / 2], BL[q / 2]);
     });
 
     // ---- hidden layers: 3 f16 MFMAs per fp32 product ----
-    const int nblocks = nh * NB;
-    int J = 0;
+    int J = 0, slot = 0;
     for (int layer = 1; layer <= nh; ++layer) {
         const bool last = layer == nh;
         const float s = p.wscale[layer - 1];
         const float m = p.w0f / s;  // power-of-two scale: exact
-        // sine + split (or output-layer accumulation) of output block j, in two
-        // halves that land between the MFMAs of the first K-chunks of block j+1
-        float x[4];
-        auto sine = [&](int h, const f4& a) __attribute__((always_inline)) {
+        // sine + split (or output-layer accumulation) of output block j, in 2 CG
+        // pieces that land between the MFMAs of the first K-chunks of block j+1
+        float x[CG][4];
+        auto sine = [&](int c, int h, const f4& a) __attribute__((always_inline)) {
             const f2 v = sin2_cw((f2){a[2 * h], a[2 * h + 1]} * m);
-            x[2 * h] = v.x;
-            x[2 * h + 1] = v.y;
+            x[c][2 * h] = v.x;
+            x[c][2 * h + 1] = v.y;
             // pin the sine to this K-chunk (IR passes would otherwise sink every
             // block's epilogue to the layer end, keeping NB accumulators live)
-            asm volatile("" : "+v"(x[2 * h]), "+v"(x[2 * h + 1]));
+            asm volatile("" : "+v"(x[c][2 * h]), "+v"(x[c][2 * h + 1]));
         };
         auto finish = [&](auto jc) __attribute__((always_inline)) {
             constexpr int j = decltype(jc)::value;
-            if (last)
-                out_acc(j, x);
-            else {
-                split4<4 * (j & 1)>(x, NH[j / 2], NL[j / 2]);
-                constexpr int w = 2 * (j & 1);
-                asm volatile("" : "+v"(NH[j / 2].w[w]), "+v"(NH[j / 2].w[w + 1]), "+v"(NL[j / 2].w[w]),
-                             "+v"(NL[j / 2].w[w + 1]));
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                if (last)
+                    out_acc(c, j, x[c]);
+                else {
+                    split4<4 * (j & 1)>(x[c], NH[c][j / 2], NL[c][j / 2]);
+                    constexpr int w = 2 * (j & 1);
+                    asm volatile("" : "+v"(NH[c][j / 2].w[w]), "+v"(NH[c][j / 2].w[w + 1]),
+                                 "+v"(NL[c][j / 2].w[w]), "+v"(NL[c][j / 2].w[w + 1]));
+                }
             }
         };
-        constexpr int QS1 = NQ > 1 ? 1 : 0, QFIN = NQ > 2 ? 2 : NQ - 1;
-        f4 prev;
+        constexpr int NS = 2 * CG;                      // sine pieces per block
+        constexpr int QFIN = NQ - 1 < NS ? NQ - 1 : NS;  // K-chunk that finishes block j-1
+        f4 prev[CG];
         static_for<NB>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            if (J + 1 < nblocks) siren_issue_block<NB, WAVES>(p.wimg, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
-            const float* wb = wbuf + (J & 1) * BLK;
-            f4 a = *(const f4*)(film + layer * H + 16 * j + 4 * g) * s;
+            // refill the slot block J-1 used (every wave left it at the last barrier)
+            const int fill = slot == 0 ? RING - 1 : slot - 1;
+            const bool steady = J + RING - 1 < nblocks;
+            if (steady && !NOSYNC) siren_issue_block<NB, WAVES>(p.wimg, J + RING - 1, wbuf + fill * BLK, wave, lane);
+            const float* wb = wbuf + slot * BLK;
+            const f4 f = *(const f4*)(film + layer * H + 16 * j + 4 * g) * s;
+            f4 a[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) a[c] = f;
             h8 ah = *(const h8*)(wb + lane * 4);
             h8 al = *(const h8*)(wb + 256 + lane * 4);
             static_for<NQ>([&](auto qc) {
@@ -212,12 +246,16 @@ __global__ __launch_bounds__(64 * WAVES, 2) void siren_fused_split(SirenArgs p) 
                     nah = *(const h8*)(wb + (q + 1) * 512 + lane * 4);
                     nal = *(const h8*)(wb + (q + 1) * 512 + 256 + lane * 4);
                 }
-                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, BH[q].v(), a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BL[q].v(), a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BH[q].v(), a, 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < CG; ++c) a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, BH[c][q].v(), a[c], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < CG; ++c) a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BL[c][q].v(), a[c], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < CG; ++c) a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BH[c][q].v(), a[c], 0, 0, 0);
                 if constexpr (j > 0) {
-                    if constexpr (q == 0) sine(0, prev);
-                    if constexpr (q == QS1) sine(1, prev);
+#pragma unroll
+                    for (int k = 0; k < NS; ++k)
+                        if ((k < QFIN ? k : QFIN) == q) sine(k >> 1, k & 1, prev[k >> 1]);
                     if constexpr (q == QFIN) finish(std::integral_constant<int, j - 1>{});
                 }
                 if constexpr (q + 1 < NQ) {
@@ -226,61 +264,103 @@ __global__ __launch_bounds__(64 * WAVES, 2) void siren_fused_split(SirenArgs p) 
                 }
                 __builtin_amdgcn_sched_barrier(0);
             });
-            prev = a;
-            // block J+1 landed (this wave's pieces); the barrier publishes every
-            // wave's pieces and retires all reads of slot J&1 before its refill
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < CG; ++c) prev[c] = a[c];
+            // block J+1 landed (this wave's pieces; the RING-2 younger blocks may
+            // stay in flight); the barrier publishes every wave's pieces and
+            // retires all reads of this slot before its refill.  A bare s_barrier:
+            // __syncthreads' LDS release fence would drain every LDS-DMA in flight.
+            if (NOSYNC) {
+                // timing experiment only (wrong results): no weight streaming, no barrier
+            } else if (steady) {
+                if (PC_HI == PC_LO || !pc_hi)
+                    __builtin_amdgcn_s_waitcnt(vmcnt_imm((RING - 2) * PC_LO));
+                else
+                    __builtin_amdgcn_s_waitcnt(vmcnt_imm((RING - 2) * PC_HI));
+            } else {
+                __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+            }
+            if (!NOSYNC) asm volatile("s_barrier" ::: "memory");
             ++J;
+            slot = slot == RING - 1 ? 0 : slot + 1;
         });
-        sine(0, prev);
-        sine(1, prev);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) sine(k >> 1, k & 1, prev[k >> 1]);
         finish(std::integral_constant<int, NB - 1>{});
         static_for<NQ>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            BH[q] = NH[q];
-            BL[q] = NL[q];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                BH[c][q] = NH[c][q];
+                BL[c][q] = NL[c][q];
+            }
         });
     }
 
     // ---- output layer (H -> c): reduce the 4 lane groups, bias, de-normalise ----
 #pragma unroll
-    for (int oc = 0; oc < 4; ++oc) {
-        float s = o[oc];
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        o[oc] = oc < p.c ? s + p.bout[oc] : 0.f;
-    }
-    if (n < p.N && g < p.c) {
-        float v = g == 0 ? o[0] : g == 1 ? o[1] : g == 2 ? o[2] : o[3];
-        if (p.ymax) {
-            const int64_t yi = n * p.ystride + g;
-            const float hi = p.ymax[yi], lo = p.ymin[yi];
-            v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
+    for (int c = 0; c < CG; ++c) {
+        float ov[4];
+#pragma unroll
+        for (int oc = 0; oc < 4; ++oc) {
+            float sum = o[c][oc];
+            sum += __shfl_xor(sum, 16);
+            sum += __shfl_xor(sum, 32);
+            ov[oc] = oc < p.c ? sum + p.bout[oc] : 0.f;
         }
-        p.out[(b * p.N + n) * p.c + g] = v;
+        const int64_t n = n0 + 16 * c;
+        if (n < p.N && g < p.c) {
+            float v = g == 0 ? ov[0] : g == 1 ? ov[1] : g == 2 ? ov[2] : ov[3];
+            if (p.ymax) {
+                const int64_t yi = n * p.ystride + g;
+                const float hi = p.ymax[yi], lo = p.ymin[yi];
+                v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
+            }
+            p.out[(b * p.N + n) * p.c + g] = v;
+        }
     }
 }
 
 namespace {
-constexpr int kSplitWaves = 8;
 
-template <int NB>
-void launch_nb(SirenArgs a, int b, hipStream_t st) {
+int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : dflt;
+    return v >= lo && v <= hi ? v : dflt;
+}
+
+template <int NB, int RING, int CG, bool NOSYNC = false>
+void launch_ring(SirenArgs a, int b, hipStream_t st) {
     constexpr int H = NB * 16;
-    const size_t lds = sizeof(float) * ((size_t)2 * NB * 256 + (size_t)(a.nh + 1) * H + 8 * H);
-    const void* fn = (const void*)siren_fused_split<NB, kSplitWaves>;
+    constexpr int WAVES = CG == 1 ? 8 : 4;
+    const size_t lds = sizeof(float) * ((size_t)RING * NB * 256 + (size_t)(a.nh + 1) * H + 8 * H);
+    const void* fn = (const void*)siren_fused_split<NB, WAVES, RING, CG, NOSYNC>;
     CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the split-f16 decoder's LDS staging");
     CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const int64_t tiles = ceil_div(a.N, 16 * kSplitWaves);
+    const int64_t tiles = ceil_div(a.N, 16 * CG * WAVES);
     CFD_REQUIRE(tiles <= 0x7fffffff, CFD_EARG, "too many coordinates for one launch");
     for (int64_t b0 = 0; b0 < b; b0 += 65535) {
         a.b0 = b0;
         const int nb = (int)std::min<int64_t>(65535, b - b0);
-        hipLaunchKernelGGL((siren_fused_split<NB, kSplitWaves>), dim3((unsigned)tiles, nb), dim3(64 * kSplitWaves),
-                           lds, st, a);
+        hipLaunchKernelGGL((siren_fused_split<NB, WAVES, RING, CG, NOSYNC>), dim3((unsigned)tiles, nb),
+                           dim3(64 * WAVES), lds, st, a);
         check_launch("siren_fused_split");
     }
+}
+
+template <int NB>
+void launch_nb(SirenArgs a, int b, hipStream_t st) {
+    static const int cg = env_int("CFD_SIREN_SPLIT_CG", 1, 1, 2);
+    static const int ring0 = env_int("CFD_SIREN_RING", 2, 2, 3);
+    // a deeper ring needs more LDS: fall back to 2 slots when the FiLM table is large
+    const size_t film = (size_t)(a.nh + 1) * NB * 16 + 8 * NB * 16;
+    const int ring = sizeof(float) * ((size_t)ring0 * NB * 256 + film) > 160 * 1024 ? 2 : ring0;
+    if constexpr (NB == 24) {  // timing experiment (wrong results): CFD_SIREN_NOSYNC=1
+        static const int nosync = env_int("CFD_SIREN_NOSYNC", 0, 0, 1);
+        if (nosync) return cg == 1 ? launch_ring<NB, 2, 1, true>(a, b, st) : launch_ring<NB, 2, 2, true>(a, b, st);
+    }
+    if (cg == 1) return ring == 3 ? launch_ring<NB, 3, 1>(a, b, st) : launch_ring<NB, 2, 1>(a, b, st);
+    return ring == 3 ? launch_ring<NB, 3, 2>(a, b, st) : launch_ring<NB, 2, 2>(a, b, st);
 }
 }  // namespace
 
