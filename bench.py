@@ -16,7 +16,8 @@ Prints ONE JSON line (rank 0) with the driver contract plus a ``roofline`` objec
 for the dominant kernel (the CNF decoder, timed with HIP events on its stream) and
 a ``cpu_baseline`` measured on this host's cores with the oracle (rank 0, N=1).
 
-The decoder's hidden layers run by default as split-f16 (siren_fused_split: three
+The U-Net convolutions (split_f16 conv_gemm) and the decoder's hidden layers run by
+default as split-f16 (siren_fused_split: three
 f16 MFMAs per fp32 product on 22-bit operand splits, fp32-level error against an
 fp64 evaluation -- tests/test_gpu_siren_split.py); its roofline is the f16 dense
 MFMA peak / 3.  ``--siren-compute f32`` runs the exact fp32 MFMA chain
@@ -78,7 +79,7 @@ def unet_flops_per_sample():
     return 68.61e9
 
 
-def setup(dev, siren_compute="split_f16"):
+def setup(dev, siren_compute="split_f16", unet_compute="split_f16"):
     from confild_amd import synth
     from confild_amd.nf_networks import SIRENAutodecoder_film
     from confild_amd.normalize import Normalizer_ts
@@ -88,6 +89,7 @@ def setup(dev, siren_compute="split_f16"):
     sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in model.state_dict().items()})
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model.to(dev)
+    model.set_compute(unet_compute)
     diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=STEPS)
     c = CNF
     nf = SIRENAutodecoder_film(c["d"], c["L"], c["c"], c["nh"], c["H"])
@@ -181,6 +183,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--siren-compute", choices=["split_f16", "f32"], default="split_f16")
+    ap.add_argument("--unet-compute", choices=["split_f16", "fp32"], default="split_f16")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,7 +196,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    objs = setup(dev, args.siren_compute)
+    objs = setup(dev, args.siren_compute, args.unet_compute)
     mode = objs[2].compute_mode(dev)
     kname, peak, peak_basis, _ = ROOFLINE[mode]
 
@@ -238,7 +241,9 @@ def main():
             "value": value, "unit": "fields/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded weights and inputs; no checkpoints)",
-            "compute": {"unet": "fp32 (v_mfma_f32_16x16x4_f32)",
+            "compute": {"unet": ("fp32 via split-f16 convolutions (3x v_mfma_f32_16x16x32_f16 on 22-bit operand "
+                                 "splits; error vs fp64 = fp32's, DESIGN.md K1s); GroupNorm/softmax/attention fp32"
+                                 if objs[0].compute == "split_f16" else "fp32 (v_mfma_f32_16x16x4_f32)"),
                         "cnf_decoder": ("fp32 via split-f16 (3x v_mfma_f32_16x16x32_f16 on 22-bit operand "
                                         "splits; error vs fp64 = fp32's, DESIGN.md K7s)" if mode == "split_f16"
                                         else "fp32 (v_mfma_f32_16x16x4_f32)")},

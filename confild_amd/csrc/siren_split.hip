@@ -33,29 +33,38 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 namespace cfd {
 
-typedef unsigned u4 __attribute__((ext_vector_type(4)));
-
-// One MFMA operand (8 x f16) kept as 4 packed 32-bit words: writing a word is one
-// VGPR write (element inserts into an h8 value turn into v_perm chains).
+// One MFMA operand (8 x f16) as 4 packed 32-bit words, always written whole (a
+// partial write of a register tuple makes the allocator copy the tuple around).
 struct Frag {
-    unsigned w[4];
-    __device__ __forceinline__ h8 v() const { return __builtin_bit_cast(h8, (u4){w[0], w[1], w[2], w[3]}); }
+    u4 v;
+    __device__ __forceinline__ h8 h() const { return __builtin_bit_cast(h8, v); }
 };
 
-// x (4 fp32) -> f16 hi/lo halves at positions [T, T+4) of (hi, lo): RNE both times
-template <int T>
-__device__ __forceinline__ void split4(const float (&x)[4], Frag& hi, Frag& lo) {
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, h2));
+}
+
+// Operand split of the 8 values of K-chunk q (x0: output block 2q, x1: block
+// 2q+1): hi = f16(x), lo = f16(x - hi), both RNE; written as whole fragments and
+// pinned here (IR passes would otherwise sink the split to the fragment's use in
+// the next layer, keeping the fp32 values live instead).
+__device__ __forceinline__ void split8(const float (&x0)[4], const float (&x1)[4], Frag& hi, Frag& lo) {
+    unsigned hw[4], lw[4];
 #pragma unroll
-    for (int r = 0; r < 4; r += 2) {
-        const h2 h = __builtin_convertvector((f2){x[r], x[r + 1]}, h2);
-        const f2 hf = __builtin_convertvector(h, f2);
-        const h2 l = __builtin_convertvector((f2){x[r] - hf.x, x[r + 1] - hf.y}, h2);
-        hi.w[(T + r) / 2] = __builtin_bit_cast(unsigned, h);
-        lo.w[(T + r) / 2] = __builtin_bit_cast(unsigned, l);
+    for (int w = 0; w < 4; ++w) {
+        const float a = w < 2 ? x0[2 * w] : x1[2 * w - 4];
+        const float b = w < 2 ? x0[2 * w + 1] : x1[2 * w - 3];
+        hw[w] = pk_f16(a, b);
+        const f2 hf = __builtin_convertvector(__builtin_bit_cast(h2, hw[w]), f2);
+        lw[w] = pk_f16(a - hf.x, b - hf.y);
     }
+    hi.v = (u4){hw[0], hw[1], hw[2], hw[3]};
+    lo.v = (u4){lw[0], lw[1], lw[2], lw[3]};
+    asm volatile("" : "+v"(hi.v), "+v"(lo.v));
 }
 
 // sin(x) for two lanes' values on packed fp32 math (v_pk_fma_f32 / v_pk_mul_f32
@@ -90,17 +99,20 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >
 
 // CG column groups of 16 coordinates per wave share every A-fragment read (CG = 2:
 // one wave per SIMD, 512 registers; CG = 1: two waves per SIMD, 256 registers).
-template <int NB, int WAVES, int RING, int CG, bool NOSYNC = false>
+// RB output blocks (16 rows each) per LDS ring slot: one barrier per RB blocks.
+template <int NB, int WAVES, int RING, int CG, int RB = 1, bool NOSYNC = false>
 __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split(SirenArgs p) {
     static_assert(NB % 2 == 0, "split-f16 chain needs H % 32 == 0");
     constexpr int NQ = NB / 2;
     constexpr int TILE = 16 * CG * WAVES;
     constexpr int H = NB * 16;
-    constexpr int BLK = NB * 256;  // floats per block slot: NQ x (hi, lo) x 512 halves
+    constexpr int BLK = NB * 256;  // floats per output block: NQ x (hi, lo) x 512 halves
+    constexpr int SLOT = RB * BLK;
+    static_assert(NB % RB == 0, "ring slots hold whole groups of RB blocks");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int nh = p.nh;
-    float* wbuf = smem;                  // RING slots
-    float* film = smem + RING * BLK;     // (nh+1) x H
+    float* wbuf = smem;                  // RING slots of RB blocks
+    float* film = smem + RING * SLOT;    // (nh+1) x H; hidden layers' rows pre-scaled by s_i
     float* w0s = film + (nh + 1) * H;    // (H, 4)
     float* wos = w0s + 4 * H;            // (4, H) output weights
 
@@ -114,7 +126,11 @@ __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split
     {
         const float* fsrc = p.film + b * (int64_t)(nh + 1) * H;
         const int nf = (nh + 1) * H;
-        for (int i = threadIdx.x * 4; i < nf; i += 64 * WAVES * 4) *(f4*)(film + i) = *(const f4*)(fsrc + i);
+        for (int i = threadIdx.x * 4; i < nf; i += 64 * WAVES * 4) {
+            const int layer = i / H;  // H constexpr
+            const float sc = layer == 0 ? 1.0f : p.wscale[layer - 1];
+            *(f4*)(film + i) = *(const f4*)(fsrc + i) * sc;  // power-of-two: exact
+        }
     }
     for (int f = threadIdx.x; f < H; f += 64 * WAVES) {
         f4 w = {0.f, 0.f, 0.f, 0.f};
@@ -139,12 +155,12 @@ __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split
     }
 
     __syncthreads();
-    const int nblocks = nh * NB;  // nh >= 1 (host-checked)
+    const int nslots = nh * NB / RB;  // ring fills per decode (nh >= 1, host-checked)
     for (int k = 0; k < RING - 1; ++k)
-        if (k < nblocks) siren_issue_block<NB, WAVES>(p.wimg, k, wbuf + k * BLK, wave, lane);
-    // LDS-DMA pieces this wave issues per block (the in-flight count its vmcnt waits see)
-    constexpr int PC_LO = NB / WAVES, PC_HI = (NB + WAVES - 1) / WAVES;
-    const bool pc_hi = wave < NB % WAVES;
+        if (k < nslots) siren_issue_block<RB * NB, WAVES>(p.wimg, k, wbuf + k * SLOT, wave, lane);
+    // LDS-DMA pieces this wave issues per slot (the in-flight count its vmcnt waits see)
+    constexpr int PC_LO = RB * NB / WAVES, PC_HI = (RB * NB + WAVES - 1) / WAVES;
+    const bool pc_hi = wave < (RB * NB) % WAVES;
 
     Frag BH[CG][NQ], BL[CG][NQ], NH[CG][NQ], NL[CG][NQ];
     float o[CG][4];
@@ -167,100 +183,114 @@ __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split
     };
 
     // ---- layer 0 (d -> H, fp32 VALU): x = sin(w0 (W0 c + F_0)) ----
-    static_for<NB>([&](auto qc) {
+    static_for<NQ>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
-        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
 #pragma unroll
         for (int c = 0; c < CG; ++c) {
-            float u[4], x[4];
+            float x[2][4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
-                float a = cn[c][0] * w[0];
+            for (int hb = 0; hb < 2; ++hb) {
+                const int blk = 2 * q + hb;
+                const f4 fv = *(const f4*)(film + 16 * blk + 4 * g);
+                float u[4];
 #pragma unroll
-                for (int k = 1; k < 4; ++k)
-                    if (k < p.d) a = fmaf(cn[c][k], w[k], a);
-                u[r] = p.w0f * (a + fv[r]);
+                for (int r = 0; r < 4; ++r) {
+                    const f4 w = *(const f4*)(w0s + 4 * (16 * blk + 4 * g + r));
+                    float a = cn[c][0] * w[0];
+#pragma unroll
+                    for (int k = 1; k < 4; ++k)
+                        if (k < p.d) a = fmaf(cn[c][k], w[k], a);
+                    u[r] = p.w0f * (a + fv[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r += 2) {
+                    const f2 v = sin2_cw((f2){u[r], u[r + 1]});
+                    x[hb][r] = v.x;
+                    x[hb][r + 1] = v.y;
+                }
             }
-#pragma unroll
-            for (int r = 0; r < 4; r += 2) {
-                const f2 v = sin2_cw((f2){u[r], u[r + 1]});
-                x[r] = v.x;
-                x[r + 1] = v.y;
-            }
-            split4<4 * (q & 1)>(x, BH[c][q / 2], BL[c][q / 2]);
+            split8(x[0], x[1], BH[c][q], BL[c][q]);
         }
     });
 
     // ---- hidden layers: 3 f16 MFMAs per fp32 product ----
+    // Output block j's MFMAs overlap the epilogue of block j-1: its sines in
+    // K-chunk 0, and (for odd j-1) the split of blocks (j-2, j-1) into next-layer
+    // fragment j/2-1 in K-chunk 1 -- or, in the last layer, the output-layer
+    // accumulation.
     int J = 0, slot = 0;
+    constexpr int QE = NQ > 1 ? 1 : 0;  // K-chunk of the split / output step
     for (int layer = 1; layer <= nh; ++layer) {
         const bool last = layer == nh;
-        const float s = p.wscale[layer - 1];
-        const float m = p.w0f / s;  // power-of-two scale: exact
-        // sine + split (or output-layer accumulation) of output block j, in 2 CG
-        // pieces that land between the MFMAs of the first K-chunks of block j+1
-        float x[CG][4];
-        auto sine = [&](int c, int h, const f4& a) __attribute__((always_inline)) {
-            const f2 v = sin2_cw((f2){a[2 * h], a[2 * h + 1]} * m);
-            x[c][2 * h] = v.x;
-            x[c][2 * h + 1] = v.y;
-            // pin the sine to this K-chunk (IR passes would otherwise sink every
-            // block's epilogue to the layer end, keeping NB accumulators live)
-            asm volatile("" : "+v"(x[c][2 * h]), "+v"(x[c][2 * h + 1]));
+        const float m = p.w0f / p.wscale[layer - 1];  // power-of-two scale: exact
+        float x[CG][4], xs[CG][4];
+        auto sines = [&](const f4 (&a)[CG]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                const f2 v0 = sin2_cw((f2){a[c][0], a[c][1]} * m);
+                const f2 v1 = sin2_cw((f2){a[c][2], a[c][3]} * m);
+                x[c][0] = v0.x;
+                x[c][1] = v0.y;
+                x[c][2] = v1.x;
+                x[c][3] = v1.y;
+                asm volatile("" : "+v"(x[c][0]), "+v"(x[c][1]), "+v"(x[c][2]), "+v"(x[c][3]));
+            }
         };
-        auto finish = [&](auto jc) __attribute__((always_inline)) {
+        auto epilogue = [&](auto jc) __attribute__((always_inline)) {  // block j's sines are in x
             constexpr int j = decltype(jc)::value;
 #pragma unroll
             for (int c = 0; c < CG; ++c) {
-                if (last)
+                if (last) {
                     out_acc(c, j, x[c]);
-                else {
-                    split4<4 * (j & 1)>(x[c], NH[c][j / 2], NL[c][j / 2]);
-                    constexpr int w = 2 * (j & 1);
-                    asm volatile("" : "+v"(NH[c][j / 2].w[w]), "+v"(NH[c][j / 2].w[w + 1]),
-                                 "+v"(NL[c][j / 2].w[w]), "+v"(NL[c][j / 2].w[w + 1]));
+                } else if constexpr (j & 1) {
+                    split8(xs[c], x[c], NH[c][j / 2], NL[c][j / 2]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xs[c][r] = x[c][r];
                 }
             }
         };
-        constexpr int NS = 2 * CG;                      // sine pieces per block
-        constexpr int QFIN = NQ - 1 < NS ? NQ - 1 : NS;  // K-chunk that finishes block j-1
         f4 prev[CG];
         static_for<NB>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            // refill the slot block J-1 used (every wave left it at the last barrier)
-            const int fill = slot == 0 ? RING - 1 : slot - 1;
-            const bool steady = J + RING - 1 < nblocks;
-            if (steady && !NOSYNC) siren_issue_block<NB, WAVES>(p.wimg, J + RING - 1, wbuf + fill * BLK, wave, lane);
-            const float* wb = wbuf + slot * BLK;
-            const f4 f = *(const f4*)(film + layer * H + 16 * j + 4 * g) * s;
+            // at a slot's first block: refill the slot the previous group used
+            // (every wave left it at the last barrier)
+            // (one block of the group per output block, spreading the DMA issue)
+            const bool steady = J + RING - 1 < nslots;
+            {
+                const int fill = slot == 0 ? RING - 1 : slot - 1;
+                if (steady && !NOSYNC)
+                    siren_issue_block<NB, WAVES>(p.wimg, (J + RING - 1) * RB + j % RB,
+                                                 wbuf + fill * SLOT + (j % RB) * BLK, wave, lane);
+            }
+            const float* wb = wbuf + slot * SLOT + (j % RB) * BLK;
             f4 a[CG];
+            {
+                const f4 f = *(const f4*)(film + layer * H + 16 * j + 4 * g);
 #pragma unroll
-            for (int c = 0; c < CG; ++c) a[c] = f;
-            h8 ah = *(const h8*)(wb + lane * 4);
-            h8 al = *(const h8*)(wb + 256 + lane * 4);
+                for (int c = 0; c < CG; ++c) a[c] = f;
+            }
+            h8 FH[NQ], FL[NQ];
+            FH[0] = *(const h8*)(wb + lane * 4);
+            FL[0] = *(const h8*)(wb + 256 + lane * 4);
             static_for<NQ>([&](auto qc) {
                 constexpr int q = decltype(qc)::value;
-                h8 nah, nal;
                 if constexpr (q + 1 < NQ) {
-                    nah = *(const h8*)(wb + (q + 1) * 512 + lane * 4);
-                    nal = *(const h8*)(wb + (q + 1) * 512 + 256 + lane * 4);
+                    FH[q + 1] = *(const h8*)(wb + (q + 1) * 512 + lane * 4);
+                    FL[q + 1] = *(const h8*)(wb + (q + 1) * 512 + 256 + lane * 4);
                 }
 #pragma unroll
-                for (int c = 0; c < CG; ++c) a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, BH[c][q].v(), a[c], 0, 0, 0);
+                for (int c = 0; c < CG; ++c)
+                    a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(FL[q], BH[c][q].h(), a[c], 0, 0, 0);
 #pragma unroll
-                for (int c = 0; c < CG; ++c) a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BL[c][q].v(), a[c], 0, 0, 0);
+                for (int c = 0; c < CG; ++c)
+                    a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(FH[q], BL[c][q].h(), a[c], 0, 0, 0);
 #pragma unroll
-                for (int c = 0; c < CG; ++c) a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, BH[c][q].v(), a[c], 0, 0, 0);
+                for (int c = 0; c < CG; ++c)
+                    a[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(FH[q], BH[c][q].h(), a[c], 0, 0, 0);
                 if constexpr (j > 0) {
-#pragma unroll
-                    for (int k = 0; k < NS; ++k)
-                        if ((k < QFIN ? k : QFIN) == q) sine(k >> 1, k & 1, prev[k >> 1]);
-                    if constexpr (q == QFIN) finish(std::integral_constant<int, j - 1>{});
-                }
-                if constexpr (q + 1 < NQ) {
-                    ah = nah;
-                    al = nal;
+                    if constexpr (q == 0) sines(prev);
+                    if constexpr (q == QE) epilogue(std::integral_constant<int, j - 1>{});
                 }
                 __builtin_amdgcn_sched_barrier(0);
             });
@@ -270,23 +300,24 @@ __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split
             // stay in flight); the barrier publishes every wave's pieces and
             // retires all reads of this slot before its refill.  A bare s_barrier:
             // __syncthreads' LDS release fence would drain every LDS-DMA in flight.
-            if (NOSYNC) {
-                // timing experiment only (wrong results): no weight streaming, no barrier
-            } else if (steady) {
-                if (PC_HI == PC_LO || !pc_hi)
-                    __builtin_amdgcn_s_waitcnt(vmcnt_imm((RING - 2) * PC_LO));
-                else
-                    __builtin_amdgcn_s_waitcnt(vmcnt_imm((RING - 2) * PC_HI));
-            } else {
-                __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+            if constexpr (j % RB == RB - 1) {
+                if (NOSYNC) {
+                    // timing experiment only (wrong results): no weight streaming, no barrier
+                } else if (steady) {
+                    if (PC_HI == PC_LO || !pc_hi)
+                        __builtin_amdgcn_s_waitcnt(vmcnt_imm((RING - 2) * PC_LO));
+                    else
+                        __builtin_amdgcn_s_waitcnt(vmcnt_imm((RING - 2) * PC_HI));
+                } else {
+                    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+                }
+                if (!NOSYNC) asm volatile("s_barrier" ::: "memory");
+                ++J;
+                slot = slot == RING - 1 ? 0 : slot + 1;
             }
-            if (!NOSYNC) asm volatile("s_barrier" ::: "memory");
-            ++J;
-            slot = slot == RING - 1 ? 0 : slot + 1;
         });
-#pragma unroll
-        for (int k = 0; k < NS; ++k) sine(k >> 1, k & 1, prev[k >> 1]);
-        finish(std::integral_constant<int, NB - 1>{});
+        sines(prev);
+        epilogue(std::integral_constant<int, NB - 1>{});
         static_for<NQ>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
 #pragma unroll
@@ -329,12 +360,12 @@ int env_int(const char* name, int dflt, int lo, int hi) {
     return v >= lo && v <= hi ? v : dflt;
 }
 
-template <int NB, int RING, int CG, bool NOSYNC = false>
+template <int NB, int RING, int CG, int RB = 1, bool NOSYNC = false>
 void launch_ring(SirenArgs a, int b, hipStream_t st) {
     constexpr int H = NB * 16;
     constexpr int WAVES = CG == 1 ? 8 : 4;
-    const size_t lds = sizeof(float) * ((size_t)RING * NB * 256 + (size_t)(a.nh + 1) * H + 8 * H);
-    const void* fn = (const void*)siren_fused_split<NB, WAVES, RING, CG, NOSYNC>;
+    const size_t lds = sizeof(float) * ((size_t)RING * RB * NB * 256 + (size_t)(a.nh + 1) * H + 8 * H);
+    const void* fn = (const void*)siren_fused_split<NB, WAVES, RING, CG, RB, NOSYNC>;
     CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the split-f16 decoder's LDS staging");
     CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t tiles = ceil_div(a.N, 16 * CG * WAVES);
@@ -342,7 +373,7 @@ void launch_ring(SirenArgs a, int b, hipStream_t st) {
     for (int64_t b0 = 0; b0 < b; b0 += 65535) {
         a.b0 = b0;
         const int nb = (int)std::min<int64_t>(65535, b - b0);
-        hipLaunchKernelGGL((siren_fused_split<NB, WAVES, RING, CG, NOSYNC>), dim3((unsigned)tiles, nb),
+        hipLaunchKernelGGL((siren_fused_split<NB, WAVES, RING, CG, RB, NOSYNC>), dim3((unsigned)tiles, nb),
                            dim3(64 * WAVES), lds, st, a);
         check_launch("siren_fused_split");
     }
@@ -351,16 +382,17 @@ void launch_ring(SirenArgs a, int b, hipStream_t st) {
 template <int NB>
 void launch_nb(SirenArgs a, int b, hipStream_t st) {
     static const int cg = env_int("CFD_SIREN_SPLIT_CG", 1, 1, 2);
-    static const int ring0 = env_int("CFD_SIREN_RING", 2, 2, 3);
-    // a deeper ring needs more LDS: fall back to 2 slots when the FiLM table is large
+    static const int rb = env_int("CFD_SIREN_RB", 1, 1, 2);
     const size_t film = (size_t)(a.nh + 1) * NB * 16 + 8 * NB * 16;
-    const int ring = sizeof(float) * ((size_t)ring0 * NB * 256 + film) > 160 * 1024 ? 2 : ring0;
+    const bool fits2 = sizeof(float) * ((size_t)2 * 2 * NB * 256 + film) <= 160 * 1024;
     if constexpr (NB == 24) {  // timing experiment (wrong results): CFD_SIREN_NOSYNC=1
         static const int nosync = env_int("CFD_SIREN_NOSYNC", 0, 0, 1);
-        if (nosync) return cg == 1 ? launch_ring<NB, 2, 1, true>(a, b, st) : launch_ring<NB, 2, 2, true>(a, b, st);
+        if (nosync) return cg == 1 ? launch_ring<NB, 2, 1, 1, true>(a, b, st) : launch_ring<NB, 2, 2, 1, true>(a, b, st);
     }
-    if (cg == 1) return ring == 3 ? launch_ring<NB, 3, 1>(a, b, st) : launch_ring<NB, 2, 1>(a, b, st);
-    return ring == 3 ? launch_ring<NB, 3, 2>(a, b, st) : launch_ring<NB, 2, 2>(a, b, st);
+    // two groups of two blocks per slot when the LDS holds them, else one block per slot
+    if (rb == 2 && fits2)
+        return cg == 1 ? launch_ring<NB, 2, 1, 2>(a, b, st) : launch_ring<NB, 2, 2, 2>(a, b, st);
+    return cg == 1 ? launch_ring<NB, 2, 1, 1>(a, b, st) : launch_ring<NB, 2, 2, 1>(a, b, st);
 }
 }  // namespace
 

@@ -26,6 +26,7 @@ struct UParam {
     bool set = false;
     int tpack = 0;       // input-gradient pack: 0 none, 1 transposed (Cin, taps, Cout), 2 upsample 4x4 (Cin, 16, Cout)
     size_t toffset = 0;  // floats into the transposed arena
+    float split_inv = 1.f;  // split compute: 1 / s, s = power-of-two scale of this conv weight
 };
 
 struct ResSpec {
@@ -65,7 +66,9 @@ struct cfd_unet {
     float* arena_t = nullptr; // transposed conv weights (input-gradient path)
     size_t arena_t_floats = 0;
     uint16_t* arena_bf = nullptr;  // bf16 copy of the conv weights, same offsets as arena
-    int compute = CFD_COMPUTE_F32;
+    uint16_t* arena_hi = nullptr;  // split compute: f16 hi / lo parts of the scaled conv weights
+    uint16_t* arena_lo = nullptr;
+    int compute = CFD_COMPUTE_SPLIT_F16;
 };
 
 namespace {
@@ -211,12 +214,23 @@ void build(cfd_unet* h) {
     h->arena_t_floats = toff;
 }
 
-// bf16 copy of a packed conv weight, or null in fp32 compute
+// bf16 copy (bf16 compute) / f16 hi part (split compute) of a packed conv weight,
+// or null in fp32 compute
 const void* PB(const cfd_unet* h, const std::string& key) {
-    if (h->compute != CFD_COMPUTE_BF16) return nullptr;
+    if (h->compute == CFD_COMPUTE_F32) return nullptr;
     auto it = h->index.find(key);
     CFD_REQUIRE(it != h->index.end(), CFD_EKEY, "internal: missing param " + key);
-    return h->arena_bf + h->params[it->second].offset;
+    return (h->compute == CFD_COMPUTE_BF16 ? h->arena_bf : h->arena_hi) + h->params[it->second].offset;
+}
+
+// split compute: f16 lo part and 1/s of a packed conv weight (null / 1 otherwise)
+const void* PL(const cfd_unet* h, const std::string& key, float* inv) {
+    *inv = 1.f;
+    if (h->compute != CFD_COMPUTE_SPLIT_F16) return nullptr;
+    auto it = h->index.find(key);
+    CFD_REQUIRE(it != h->index.end(), CFD_EKEY, "internal: missing param " + key);
+    *inv = h->params[it->second].split_inv;
+    return h->arena_lo + h->params[it->second].offset;
 }
 
 // fp32 -> bf16, round to nearest even (what v_cvt_pk_bf16_f32 does on the device)
@@ -405,6 +419,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         a.Ctot = in.C();
         a.w = P(h, pre + ".weight");
         a.wbf = PB(h, pre + ".weight");
+        a.wlo = PL(h, pre + ".weight", &a.acc_scale);
         a.bias = P(h, pre + ".bias");
         a.emb = embp;
         a.emb_stride = h->emb_total;
@@ -765,6 +780,9 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             CFD_HIP(hipMalloc(&h->emb_b, sizeof(float) * (size_t)h->emb_total));
             CFD_HIP(hipMalloc(&h->arena_t, sizeof(float) * std::max<size_t>(h->arena_t_floats, 4)));
             CFD_HIP(hipMalloc(&h->arena_bf, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
+            CFD_HIP(hipMalloc(&h->arena_hi, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
+            CFD_HIP(hipMalloc(&h->arena_lo, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
+            if (const char* e = getenv("CFD_UNET_COMPUTE")) h->compute = atoi(e);
             const int half = cfg->model_channels / 2;
             // freqs = exp(-ln(10000) * arange(half, fp32) / half) in fp32 (nn.py:129-131)
             std::vector<float> fr(half);
@@ -788,6 +806,8 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->freqs);
     (void)hipFree(h->arena_t);
     (void)hipFree(h->arena_bf);
+    (void)hipFree(h->arena_hi);
+    (void)hipFree(h->arena_lo);
     delete h;
 }
 
@@ -836,6 +856,21 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
                 std::vector<uint16_t> bf(n);
                 for (size_t e = 0; e < n; ++e) bf[e] = to_bf16(pk[e]);
                 CFD_HIP(hipMemcpy(h->arena_bf + p.offset, bf.data(), n * 2, hipMemcpyHostToDevice));
+                // split compute: s w = wh + wl, s = 2^-e with e the frexp exponent of max|w|
+                float amax = 0.f;
+                for (size_t e = 0; e < n; ++e) amax = std::max(amax, std::fabs(pk[e]));
+                int ex = 0;
+                if (amax > 0.f) std::frexp(amax, &ex);
+                const float s = std::ldexp(1.0f, -ex);
+                p.split_inv = std::ldexp(1.0f, ex);
+                std::vector<_Float16> hi(n), lo(n);
+                for (size_t e = 0; e < n; ++e) {
+                    const float v = pk[e] * s;
+                    hi[e] = (_Float16)v;
+                    lo[e] = (_Float16)(v - (float)hi[e]);
+                }
+                CFD_HIP(hipMemcpy(h->arena_hi + p.offset, hi.data(), n * 2, hipMemcpyHostToDevice));
+                CFD_HIP(hipMemcpy(h->arena_lo + p.offset, lo.data(), n * 2, hipMemcpyHostToDevice));
                 break;
             }
             case Pack::EmbW:
@@ -881,7 +916,8 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
 extern "C" int cfd_unet_set_compute(cfd_unet* h, int compute) {
     return cfd::guard([&] {
         CFD_REQUIRE(h, CFD_EARG, "null handle");
-        CFD_REQUIRE(compute == CFD_COMPUTE_F32 || compute == CFD_COMPUTE_BF16, CFD_EARG, "unknown compute mode");
+        CFD_REQUIRE(compute == CFD_COMPUTE_F32 || compute == CFD_COMPUTE_BF16 || compute == CFD_COMPUTE_SPLIT_F16,
+                    CFD_EARG, "unknown compute mode");
         h->compute = compute;
     });
 }
@@ -956,8 +992,9 @@ extern "C" int cfd_unet_forward_tape(cfd_unet* h, const float* x, const int64_t*
                                      void* workspace, size_t ws_bytes, void* tape, size_t tape_bytes, void* stream) {
     return cfd::guard([&] {
         CFD_REQUIRE(h && x && t && eps && workspace && tape, CFD_EARG, "null argument");
-        CFD_REQUIRE(h->compute == CFD_COMPUTE_F32, CFD_ESTATE,
-                    "the input-gradient path is fp32: call cfd_unet_set_compute(h, CFD_COMPUTE_F32) first");
+        CFD_REQUIRE(h->compute != CFD_COMPUTE_BF16, CFD_ESTATE,
+                    "the input-gradient path is fp32-accurate: call cfd_unet_set_compute(h, CFD_COMPUTE_F32) "
+                    "or CFD_COMPUTE_SPLIT_F16 first");
         CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
         check_ready(h);
         size_t need = 0, tneed = 0;

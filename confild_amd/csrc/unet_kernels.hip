@@ -169,12 +169,22 @@ __device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 32 + 4
 // (k = 8g..8g+7, the MFMA operand layout), conflict-free.
 __device__ __forceinline__ int lds_swz_bf(int row, int chunk) { return row * 64 + ((chunk + (row >> 2)) & 3) * 16; }
 
-template <int BM, int BN, bool TMODE, bool BF>
+// SPLIT (MODE 2, default fp32 path): fp32-accurate convolution on f16 MFMA.
+// Activations are split as staged, x = xh + xl (xh = f16(x), xl = f16(x - xh),
+// RNE); weights come pre-split from the host as (s w) = wh + wl with a
+// power-of-two s per convolution (a.wbf = wh, a.wlo = wl, a.acc_scale = 1/s).
+// Each product runs as wl xh + wh xl + wh xh on v_mfma_f32_16x16x32_f16 (fp32
+// accumulate): 22-bit operands, exact products, the fp32 accumulation order of
+// the fp32 kernel -- error against fp64 at the fp32 kernel's level
+// (tests/test_gpu_unet_split.py).  hi and lo tiles use the bf16 LDS layout.
+template <int BM, int BN, bool TMODE, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
+    constexpr bool BF = MODE == 1, SP = MODE == 2;
     constexpr int BK = 32;
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 16, TN = WN / 16;
     constexpr int AIT = BM / 32, BIT = BN / 32;  // float4 (bf16: 4 x bf16) per thread per tile
+    // floats per LDS tile: fp32 BM*BK; bf16 half that; split two f16 tiles (hi, lo)
     constexpr int AFL = BF ? BM * BK / 2 : BM * BK, BFL = BF ? BN * BK / 2 : BN * BK;
     __shared__ __attribute__((aligned(16))) float As[2][AFL];
     __shared__ __attribute__((aligned(16))) float Bs[2][BFL];
@@ -209,15 +219,17 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     }
     const float* wrow[BIT];
     const unsigned short* wrow_bf[BIT];
+    const unsigned short* wrow_lo[BIT];
     bool b_ok[BIT];
 #pragma unroll
     for (int it = 0; it < BIT; ++it) {
         const int n = n0 + rsub + it * 32;
         b_ok[it] = n < a.Cout;
-        if constexpr (BF)
+        if constexpr (BF || SP)
             wrow_bf[it] = (const unsigned short*)a.wbf + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
         else
             wrow[it] = a.w + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
+        if constexpr (SP) wrow_lo[it] = (const unsigned short*)a.wlo + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
     }
     const int nkt = a.K / BK;
     const int per = (nkt + gridDim.z - 1) / gridDim.z;
@@ -235,7 +247,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
 
     const int smask = a.stride - 1, sshift = a.stride >> 1;
     f4 ra[AIT], rb[BIT];
-    uint2 rbh[BIT];
+    uint2 rbh[BIT], rbl[BIT];
     auto load_tile = [&](int kt) {
         const int c0 = cb + 4 * kq;
 #pragma unroll
@@ -270,9 +282,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
-            if constexpr (BF)
+            if constexpr (BF || SP)
                 rbh[it] = b_ok[it] ? *(const uint2*)(wrow_bf[it] + kt * BK) : uint2{0u, 0u};
-            else
+            if constexpr (SP)
+                rbl[it] = b_ok[it] ? *(const uint2*)(wrow_lo[it] + kt * BK) : uint2{0u, 0u};
+            if constexpr (!BF && !SP)
                 rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kt * BK) : f4{0.f, 0.f, 0.f, 0.f};
         }
         cb += BK;
@@ -285,7 +299,23 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         }
     };
     auto store_tile = [&](int buf) {
-        if constexpr (BF) {
+        if constexpr (SP) {
+            // hi tile at [0, BM*BK/2) floats, lo tile after it (same bf16 layout)
+#pragma unroll
+            for (int it = 0; it < AIT; ++it) {
+                const h4 hv = __builtin_convertvector(ra[it], h4);
+                const h4 lv = __builtin_convertvector(ra[it] - __builtin_convertvector(hv, f4), h4);
+                const int off = lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8;
+                *(h4*)((char*)As[buf] + off) = hv;
+                *(h4*)((char*)As[buf] + BM * BK * 2 + off) = lv;
+            }
+#pragma unroll
+            for (int it = 0; it < BIT; ++it) {
+                const int off = lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8;
+                *(uint2*)((char*)Bs[buf] + off) = rbh[it];
+                *(uint2*)((char*)Bs[buf] + BN * BK * 2 + off) = rbl[it];
+            }
+        } else if constexpr (BF) {
             // thread kq holds k = 4kq..4kq+3: chunk kq/2, half kq%2
 #pragma unroll
             for (int it = 0; it < AIT; ++it) {
@@ -317,7 +347,30 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         for (int kt = kt0; kt < kt1; ++kt) {
             const int cur = (kt - kt0) & 1;
             if (kt + 1 < kt1) load_tile(kt + 1);
-            if constexpr (BF) {
+            if constexpr (SP) {
+                const int g = lane >> 4;
+                h8v fah[TM], fal[TM], fbh[TN], fbl[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int off = lds_swz_bf(wm * WM + 16 * i + li, g);
+                    fah[i] = *(const h8v*)((const char*)As[cur] + off);
+                    fal[i] = *(const h8v*)((const char*)As[cur] + BM * BK * 2 + off);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int off = lds_swz_bf(wn * WN + 16 * j + li, g);
+                    fbh[j] = *(const h8v*)((const char*)Bs[cur] + off);
+                    fbl[j] = *(const h8v*)((const char*)Bs[cur] + BN * BK * 2 + off);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                    }
+            } else if constexpr (BF) {
                 const int g = lane >> 4;
                 bf16x8 fa[TM], fb[TN];
 #pragma unroll
@@ -353,6 +406,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     }
 
     const int g4 = 4 * (lane >> 4);
+    if constexpr (SP) {  // undo the power-of-two weight scale (exact)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] *= a.acc_scale;
+    }
     if (gridDim.z > 1) {
         float* part = a.part + (int64_t)blockIdx.z * a.M * a.Cout;
 #pragma unroll
@@ -642,16 +701,16 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     return p;
 }
 
-template <bool TMODE, bool BF>
+template <bool TMODE, int MODE>
 static void launch_conv_tiles(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
     if (p.bm == 128 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, BF>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE>), grid, dim3(256), 0, st, a);
     else if (p.bm == 64 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE, BF>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE, MODE>), grid, dim3(256), 0, st, a);
     else if (p.bm == 128 && p.bn == 64)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 64, TMODE, BF>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 64, TMODE, MODE>), grid, dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE, BF>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE, MODE>), grid, dim3(256), 0, st, a);
 }
 
 void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
@@ -662,11 +721,13 @@ void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
     CFD_REQUIRE(!(a.tmode && a.wbf), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
     if (a.tmode)
-        launch_conv_tiles<true, false>(a, p, grid, st);
+        launch_conv_tiles<true, 0>(a, p, grid, st);
+    else if (a.wbf && a.wlo)
+        launch_conv_tiles<false, 2>(a, p, grid, st);
     else if (a.wbf)
-        launch_conv_tiles<false, true>(a, p, grid, st);
+        launch_conv_tiles<false, 1>(a, p, grid, st);
     else
-        launch_conv_tiles<false, false>(a, p, grid, st);
+        launch_conv_tiles<false, 0>(a, p, grid, st);
     check_launch("conv_gemm_kernel");
     if (p.splits > 1) {
         const int64_t total4 = (int64_t)a.M * a.Cout / 4;

@@ -24,7 +24,9 @@ struct ConvArgs {
     const float* src1;
     const float* src2;   // concat-free second source (channels C1..C1+C2) or null
     const float* w;      // packed (Cout, ks*ks, Ctot)
-    const void* wbf;     // the same packing in bf16 (config E compute), or null for fp32
+    const void* wbf;     // the same packing in bf16 (config E compute) / f16 hi part (split), or null
+    const void* wlo;     // split compute: f16 lo part of the scaled weights, or null
+    float acc_scale;     // split compute: 1 / (power-of-two weight scale)
     const float* bias;   // (Cout) or null
     const float* emb;    // (B, emb_stride) slice, or null
     const float* res;    // (M, Cout) residual, or null

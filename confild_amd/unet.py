@@ -174,7 +174,9 @@ class UNetModel(nn.Module):
         self._shapes = shapes
         _build_tree(self, shapes)
         self._reset_parameters()
-        self.compute = "fp32"  # convolution operands: "fp32" (reference arithmetic) or "bf16" (config E)
+        # convolution arithmetic: "split_f16" (default; fp32-accurate on f16 MFMA, DESIGN.md
+        # K1s), "fp32" (exact fp32 MFMA) or "bf16" (bf16 operands, config E)
+        self.compute = "split_f16"
         self._handles = {}      # device index -> (handle ptr, uploaded signature)
         self._workspaces = {}   # (device, B) -> uint8 tensor
 
@@ -216,11 +218,15 @@ class UNetModel(nn.Module):
         cfg.num_head_channels = self.num_head_channels
         return cfg
 
+    COMPUTE_MODES = {"fp32": 0, "bf16": 1, "split_f16": 2}
+
     def set_compute(self, compute: str):
-        """Convolution operand precision: "fp32" (default, exact reference arithmetic) or
-        "bf16" (bf16 operands, fp32 accumulation; GroupNorm/softmax/attention stay fp32)."""
-        if compute not in ("fp32", "bf16"):
-            raise ValueError(f"compute must be 'fp32' or 'bf16', got {compute!r}")
+        """Convolution arithmetic: "fp32" (exact fp32 MFMA), "split_f16" (three f16 MFMAs on
+        22-bit operand splits: fp32-level error) or "bf16" (bf16 operands,
+        fp32 accumulation).  GroupNorm, softmax, attention and the 1-channel in/out
+        convolutions stay fp32 in every mode."""
+        if compute not in self.COMPUTE_MODES:
+            raise ValueError(f"compute must be one of {sorted(self.COMPUTE_MODES)}, got {compute!r}")
         self.compute = compute
         return self
 
@@ -251,7 +257,7 @@ class UNetModel(nn.Module):
                            f"set_param {k}")
             _lib.check(lib.cfd_unet_ready(h), "cfd_unet_ready")
             entry[1] = sig
-        _lib.check(lib.cfd_unet_set_compute(entry[0], 1 if self.compute == "bf16" else 0), "cfd_unet_set_compute")
+        _lib.check(lib.cfd_unet_set_compute(entry[0], self.COMPUTE_MODES[self.compute]), "cfd_unet_set_compute")
         return entry[0]
 
     def _workspace(self, h, device, B):
@@ -300,8 +306,9 @@ class UNetModel(nn.Module):
     def forward_tape(self, x: torch.Tensor, timesteps: torch.Tensor) -> torch.Tensor:
         """forward() that also records the activations for input_vjp (bit-identical eps)."""
         x, t, B = self._prep(x, timesteps)
-        if self.compute != "fp32":
-            raise NotImplementedError("the input-gradient (DPS) path is fp32: set_compute('fp32')")
+        if self.compute == "bf16":
+            raise NotImplementedError("the input-gradient (DPS) path is fp32-accurate: set_compute('fp32') or "
+                                      "set_compute('split_f16')")
         h = self._handle(x.device)
         lib = _lib.load()
         ws = self._workspace(h, x.device, B)

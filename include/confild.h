@@ -77,11 +77,18 @@ int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
  * CFD_COMPUTE_BF16 rounds both convolution operands to bf16 (RNE) and
  * accumulates in fp32 on v_mfma_f32_16x16x32_bf16; GroupNorm, softmax,
  * attention, the timestep MLP and the 1-channel in/out convolutions stay fp32.
- * Default CFD_COMPUTE_F32 (exact fp32, the reference's arithmetic).  This
+ * Default CFD_COMPUTE_SPLIT_F16 (fp32-accurate, below); CFD_COMPUTE_F32 is the
+ * exact fp32 MFMA path.  This
  * replaces UNetModel's use_fp16 torso conversion (U/src/unet.py:619-633) with
  * bf16 operands. */
-#define CFD_COMPUTE_F32  0
-#define CFD_COMPUTE_BF16 1
+/* CFD_COMPUTE_SPLIT_F16: fp32-accurate convolutions on f16 MFMA -- activations
+ * and power-of-two-scaled weights split into f16 hi + lo (22-bit operands),
+ * three v_mfma_f32_16x16x32_f16 per product (lo*hi + hi*lo + hi*hi), fp32
+ * accumulation; error against an fp64 evaluation at the fp32 kernel's level
+ * (DESIGN.md K1s).  Activations must stay below 65504 in magnitude. */
+#define CFD_COMPUTE_F32       0
+#define CFD_COMPUTE_BF16      1
+#define CFD_COMPUTE_SPLIT_F16 2
 int  cfd_unet_set_compute(cfd_unet* h, int compute);
 int  cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                       void* workspace, size_t ws_bytes, void* stream);

@@ -42,9 +42,14 @@ class Config:
         self.out_channels = out_channels
 
 
+def _atleast_f32(x):
+    return x if x.dtype == torch.float64 else x.float()
+
+
 def _gn(sd, pre, x):
     # GroupNorm32: 32 groups, eps 1e-5, computed in fp32 (nn.py:17-19,108-115)
-    return F.group_norm(x.float(), 32, sd[pre + ".weight"], sd[pre + ".bias"], 1e-5).type(x.dtype)
+    # GroupNorm32 runs in fp32 (nn.py:17-19); fp64 evaluations (tests) stay fp64
+    return F.group_norm(_atleast_f32(x), 32, sd[pre + ".weight"], sd[pre + ".bias"], 1e-5).type(x.dtype)
 
 
 def _conv(sd, pre, x, stride=1, pad=1):
@@ -91,7 +96,7 @@ def attention(sd, pre, x, channels, cfg: Config):
     q, k, v = qkv.reshape(bs * heads, ch * 3, length).split(ch, dim=1)
     scale = 1 / math.sqrt(math.sqrt(ch))
     w = torch.einsum("bct,bcs->bts", q * scale, k * scale)
-    w = torch.softmax(w.float(), dim=-1).type(w.dtype)
+    w = torch.softmax(_atleast_f32(w), dim=-1).type(w.dtype)
     a = torch.einsum("bts,bcs->bct", w, v).reshape(bs, -1, length)
     h = _conv1d(sd, pre + ".proj_out", a)
     return (xf + h).reshape(b, c, hh, ww)
@@ -100,7 +105,7 @@ def attention(sd, pre, x, channels, cfg: Config):
 def forward(sd: dict, cfg: Config, x: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
     """UNetModel.forward, unet.py:634-663 (topology from __init__ :427-616)."""
     mc = cfg.model_channels
-    emb = timestep_embedding(t, mc)
+    emb = timestep_embedding(t, mc).to(sd["time_embed.0.weight"].dtype)  # fp64 evaluations (tests)
     emb = F.linear(emb, sd["time_embed.0.weight"], sd["time_embed.0.bias"])
     emb = F.linear(F.silu(emb), sd["time_embed.2.weight"], sd["time_embed.2.bias"])
 

@@ -1,0 +1,64 @@
+"""Split-f16 U-Net convolutions (K1s, CFD_COMPUTE_SPLIT_F16) against an fp64
+evaluation of the reference forward (U/src/unet.py:634-663) and against the
+exact fp32 kernels, on the reference-pinned fixture inputs.
+
+The claim under test: split-f16 is an fp32-accuracy U-Net -- its error against
+fp64 is bounded by 2x the error of the fp32 HIP path (and of the fp32 CPU
+oracle) plus 1e-7 of the output scale, and it meets the 1e-4 tolerance of the
+fp32 parity tests against the reference fixtures.
+"""
+import ast
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from confild_amd import synth
+from confild_amd.script_util import create_model
+from oracle import unet as ou
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("name", ["tiny16", "small32", "heads16", "cfgA32", "cfgB64", "cfgE128"])
+def test_split_unet_has_fp32_accuracy(hip, name):
+    g = golden(f"unet_{name}.npz")
+    kw = ast.literal_eval(str(g["kwargs"]))
+    m = create_model(**kw)
+    sd = synth.unet_state_dict(int(g["seed"]), {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.to(DEV)
+    x = torch.from_numpy(g["x"])
+    t = torch.from_numpy(g["t"])
+    with torch.no_grad():
+        ref64 = ou.forward({k: torch.from_numpy(v).double() for k, v in sd.items()}, ou.Config(**kw),
+                           x.double(), t).double()
+    e_cpu = (torch.from_numpy(g["eps"]).double() - ref64).abs()
+    out = {}
+    for mode in ("fp32", "split_f16"):
+        m.set_compute(mode)
+        out[mode] = m(x.to(DEV), t.to(DEV)).cpu().double()
+    e32 = (out["fp32"] - ref64).abs()
+    esp = (out["split_f16"] - ref64).abs()
+    scale = ref64.abs().max().item()
+    print(f"{name}: max|err| vs fp64 / max|ref|: split {esp.max() / scale:.3e} fp32-HIP {e32.max() / scale:.3e} "
+          f"cpu-fp32 {e_cpu.max() / scale:.3e}; mean split {esp.mean() / scale:.3e} fp32 {e32.mean() / scale:.3e}")
+    assert esp.max().item() <= 2 * max(e32.max().item(), e_cpu.max().item()) + 1e-7 * scale
+    assert esp.mean().item() <= 2 * max(e32.mean().item(), e_cpu.mean().item()) + 1e-8 * scale
+    assert np.abs(out["split_f16"].numpy() - g["eps"]).max() / np.abs(g["eps"]).max() <= 1e-4
+
+
+def test_split_unet_batch_invariant(hip):
+    g = golden("unet_cfgB64.npz")
+    kw = ast.literal_eval(str(g["kwargs"]))
+    m = create_model(**kw)
+    sd = synth.unet_state_dict(int(g["seed"]), {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.to(DEV).set_compute("split_f16")
+    x = torch.from_numpy(synth.normal(5, "bx", (5, 1, 64, 64))).to(DEV)
+    t = torch.tensor([999, 500, 3, 0, 250], dtype=torch.int64, device=DEV)
+    eps = m(x, t)
+    for i in (0, 3):
+        assert torch.equal(m(x[i:i + 1], t[i:i + 1]), eps[i:i + 1])

@@ -57,13 +57,15 @@ def bench_siren(latents=64, npts=64 ** 3, dims=(3, 64, 3, 15, 384), iters=3, com
                       "tflops": flops / (best / 1e3) / 1e12}), flush=True)
 
 
-def bench_unet(batch=8, size=64, iters=10, bf16=False):
+def bench_unet(batch=8, size=64, iters=10, bf16=False, compute=None):
     from confild_amd.script_util import create_model
     m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
                      attention_resolutions="32,16,8", use_bf16=bf16)
     sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     m.to(DEV)
+    if compute:
+        m.set_compute(compute)
     x = torch.randn(batch, 1, size, size, device=DEV)
     t = torch.full((batch,), 500, dtype=torch.int64, device=DEV)
     med, best = timeit(lambda: m(x, t), iters=iters, warm=2)
@@ -123,11 +125,12 @@ if __name__ == "__main__":
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--compute", choices=["f32", "split_f16"], default=None)
+    ap.add_argument("--unet-compute", choices=["fp32", "split_f16", "bf16"], default=None)
     ap.add_argument("--dims", default="3,64,3,15,384", help="SIREN d,L,c,nh,H")
     a = ap.parse_args()
     if a.what in ("siren", "sweep"):
         bench_siren(a.latents, dims=tuple(int(v) for v in a.dims.split(",")), compute=a.compute)
     if a.what in ("unet", "sweep"):
-        bench_unet(a.batch, a.size, bf16=a.bf16)
+        bench_unet(a.batch, a.size, bf16=a.bf16, compute=a.unet_compute)
     if a.what == "dps":
         bench_dps(a.batch, a.size)
