@@ -479,6 +479,7 @@ struct cfd_siren {
     float* wimg_t = nullptr; // transposed weight image, layers nh..1 (latent-gradient path)
     float* wimg16 = nullptr; // split-f16 image (hi, lo) of the scaled hidden weights, same bytes as wimg
     float* wscale = nullptr; // (nh) power-of-two scale of each hidden layer in wimg16
+    float* wimg32 = nullptr; // the same split in the 32x32x16 chain's k order (siren_split32)
     int compute = CFD_SIREN_SPLIT_F16;
 };
 
@@ -563,6 +564,27 @@ void pack_split_f16(cfd_siren* h, int li, const float* W) {
                 }
     CFD_HIP(hipMemcpy(h->wimg16 + (size_t)(li - 1) * NB * NB * 256, img.data(), img.size() * sizeof(_Float16),
                       hipMemcpyHostToDevice));
+    // 32x32x16 image: block J (32 rows), K-chunk k = 2 jb + e: 1 KiB of Wh then
+    // 1 KiB of Wl, lane-linear, lane l element t =
+    // W[32J + l%32][32 jb + 8(2e + t/4) + 4(l/32) + t%4]
+    if (H % 32 == 0) {
+        const int NB2 = H / 32, NK = H / 16;
+        for (int J = 0; J < NB2; ++J)
+            for (int k = 0; k < NK; ++k)
+                for (int l = 0; l < 64; ++l)
+                    for (int t = 0; t < 8; ++t) {
+                        const int jb = k / 2, e = k % 2;
+                        const float v = W[(size_t)(32 * J + l % 32) * H + 32 * jb + 8 * (2 * e + t / 4) +
+                                          4 * (l / 32) + t % 4] * s;
+                        const _Float16 hi = (_Float16)v;
+                        const _Float16 lo = (_Float16)(v - (float)hi);
+                        const size_t base = ((size_t)J * NK + k) * 1024 + l * 8 + t;
+                        img[base] = hi;
+                        img[base + 512] = lo;
+                    }
+        CFD_HIP(hipMemcpy(h->wimg32 + (size_t)(li - 1) * NB * NB * 256, img.data(),
+                          img.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
     CFD_HIP(hipMemcpy(h->wscale + (li - 1), &s, sizeof(float), hipMemcpyHostToDevice));
 }
 
@@ -602,6 +624,7 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_HIP(hipMalloc(&h->wimg_t, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wimg16, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wscale, sizeof(float) * (size_t)std::max(nh, 1)));
+        CFD_HIP(hipMalloc(&h->wimg32, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         if (const char* e = getenv("CFD_SIREN_COMPUTE")) h->compute = atoi(e);
         *out = h;
     });
@@ -618,6 +641,7 @@ extern "C" void cfd_siren_destroy(cfd_siren* h) {
     (void)hipFree(h->wimg_t);
     (void)hipFree(h->wimg16);
     (void)hipFree(h->wscale);
+    (void)hipFree(h->wimg32);
     delete h;
 }
 
@@ -743,9 +767,18 @@ extern "C" int cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, c
         a.nh = nh;
         a.w0f = h->cfg.w0;
         if (h->compute == CFD_SIREN_SPLIT_F16 && nh >= 1 && cfd::siren_split_supported(h->NB)) {
-            a.wimg = h->wimg16;
             a.wscale = h->wscale;
-            cfd::launch_siren_split(h->NB, a, b, st);
+            static const bool use32 = [] {
+                const char* e = getenv("CFD_SIREN_SPLIT32");
+                return !e || atoi(e) != 0;
+            }();
+            if (use32 && cfd::siren_split32_supported(H, nh)) {
+                a.wimg = h->wimg32;
+                cfd::launch_siren_split32(H, a, b, st);
+            } else {
+                a.wimg = h->wimg16;
+                cfd::launch_siren_split(h->NB, a, b, st);
+            }
         } else {
             launch_siren(h, a, b, st);
         }

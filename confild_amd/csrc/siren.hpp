@@ -58,5 +58,8 @@ __device__ __forceinline__ void siren_issue_block(const float* __restrict__ wimg
 // Split-f16 chain (siren_split.hip).  Defined for even NB (H a multiple of 32).
 bool siren_split_supported(int NB);
 void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st);
+// 32x32x16 form of the chain (K7t, image from pack_split_f16_32)
+bool siren_split32_supported(int H, int nh);
+void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st);
 
 }  // namespace cfd

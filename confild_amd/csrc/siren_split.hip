@@ -94,13 +94,38 @@ __device__ __forceinline__ f2 sin2_cw(f2 x) {
     return __builtin_bit_cast(f2, __builtin_bit_cast(u2, y) + sg);
 }
 
+// Scalar form of sin2_cw (one value; same constants and result bits).  Beside
+// MFMAs a packed-fp32 instruction costs more issue than two scalar ones
+// (MI355X_MICROARCH.md, one-wave-per-SIMD filler prices), so both are kept.
+__device__ __forceinline__ float sin1_cw(float x) {
+    const float t = fmaf(x, 0.318309886183790671538f, 12582912.0f);
+    const float q = t - 12582912.0f;
+    float r = fmaf(q, -3.140625f, x);
+    r = fmaf(q, -0.0009670257568359375f, r);
+    r = fmaf(q, -6.2771141529083251953e-07f, r);
+    r = fmaf(q, -1.2154201256553420762e-10f, r);
+    const float s = r * r;
+    float u = 2.6083159809786593541503e-06f;
+    u = fmaf(u, s, -0.0001981069071916863322258f);
+    u = fmaf(u, s, 0.00833307858556509017944336f);
+    u = fmaf(u, s, -0.166666597127914428710938f);
+    const float y = fmaf(s, u * r, r);
+    return __uint_as_float(__float_as_uint(y) + (__float_as_uint(t) << 31));
+}
+
+template <bool PK>
+__device__ __forceinline__ f2 sin2_sel(f2 x) {
+    if constexpr (PK) return sin2_cw(x);
+    else return (f2){sin1_cw(x.x), sin1_cw(x.y)};
+}
+
 // s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
 constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
 
 // CG column groups of 16 coordinates per wave share every A-fragment read (CG = 2:
 // one wave per SIMD, 512 registers; CG = 1: two waves per SIMD, 256 registers).
 // RB output blocks (16 rows each) per LDS ring slot: one barrier per RB blocks.
-template <int NB, int WAVES, int RING, int CG, int RB = 1, bool NOSYNC = false>
+template <int NB, int WAVES, int RING, int CG, int RB = 1, bool NOSYNC = false, bool PKSIN = true>
 __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split(SirenArgs p) {
     static_assert(NB % 2 == 0, "split-f16 chain needs H % 32 == 0");
     constexpr int NQ = NB / 2;
@@ -227,8 +252,8 @@ __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split
         auto sines = [&](const f4 (&a)[CG]) __attribute__((always_inline)) {
 #pragma unroll
             for (int c = 0; c < CG; ++c) {
-                const f2 v0 = sin2_cw((f2){a[c][0], a[c][1]} * m);
-                const f2 v1 = sin2_cw((f2){a[c][2], a[c][3]} * m);
+                const f2 v0 = sin2_sel<PKSIN>((f2){a[c][0] * m, a[c][1] * m});
+                const f2 v1 = sin2_sel<PKSIN>((f2){a[c][2] * m, a[c][3] * m});
                 x[c][0] = v0.x;
                 x[c][1] = v0.y;
                 x[c][2] = v1.x;
@@ -352,6 +377,279 @@ __global__ __launch_bounds__(64 * WAVES, CG == 1 ? 2 : 1) void siren_fused_split
     }
 }
 
+// ---------------------------------------------------------------------------
+// K7t: the same split-f16 chain on v_mfma_f32_32x32x16_f16, one wave per SIMD.
+//
+// Why: the 16x16x32 chain above is issue-bound, not MFMA-bound.  A 16x16x32
+// MFMA holds the SIMD's vector issue for 8 of its 16 cycles, and each fp32
+// activation needs ~15 VALU instructions (scale, sine, split) -- together more
+// issue than the MFMA time they hide behind.  A 32x32x16 MFMA holds issue for 8
+// of its 32 cycles at the same FLOP rate, which halves the hold per FLOP.
+//
+// Layout: workgroup = 4 waves x 32 coordinates, one latent (grid.y).  Output
+// block J (32 features) of a layer is one 32x32 accumulator: lane (h = l/32,
+// n = l%32) holds features 32J + 8qq + 4h + r at acc[4qq + r] for coordinate n.
+// K-chunk 2J + e of the next layer (16 features) is lane-local: lane (h, n)
+// element t = acc[8e + t], feature 32J + 8(2e + t/4) + 4h + t%4 -- the weight
+// image is packed in that k order (pack_split_f16_32), so no shuffle between
+// layers.  Weights stream through a 2-slot LDS ring by LDS-DMA, one 32-row block
+// (NK x {hi, lo} x 1 KiB) per slot, issued in the first half of the previous
+// block.  Block j's MFMAs overlap block j-1's sines (one value per K-chunk step)
+// and its split (v_fma_mix: lo = f16(x - hi) in one instruction per value).
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+// hi/lo f16 split of two values: hi = f16(a, b) (RNE), lo = f16(a - hi_a, b - hi_b)
+// (a - hi is exact in fp32, so one rounding as in split8).
+__device__ __forceinline__ void split2_mix(float a, float b, unsigned& hi, unsigned& lo) {
+    hi = pk_f16(a, b);
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo) : "v"(a), "v"(hi));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo) : "v"(b), "v"(hi));
+}
+
+// chunk e (0, 1) of a 32x32 block's 16 values -> (hi, lo) fragments
+__device__ __forceinline__ void split_chunk(const float (&x)[16], int e, Frag& hi, Frag& lo) {
+    unsigned hw[4], lw[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) split2_mix(x[8 * e + 2 * w], x[8 * e + 2 * w + 1], hw[w], lw[w]);
+    hi.v = (u4){hw[0], hw[1], hw[2], hw[3]};
+    lo.v = (u4){lw[0], lw[1], lw[2], lw[3]};
+    asm volatile("" : "+v"(hi.v), "+v"(lo.v));
+}
+
+// EXP (timing experiments only, wrong results): bit 0 no weight streaming / barrier,
+// bit 1 no sine (x = scaled accumulator), bit 2 A-fragment prefetch two steps ahead
+template <int NB2, int EXP = 0>
+__global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
+    constexpr int NK = 2 * NB2;    // 16-deep K chunks per layer
+    constexpr int H = 32 * NB2;
+    constexpr int BLK = NK * 512;  // floats per 32-row block: NK x {hi, lo} x 1 KiB
+    constexpr int WAVES = 4, TILE = 128;
+    constexpr int NPC = 2 * NK;    // 1-KiB LDS-DMA pieces per block
+    constexpr int PPW = NPC / WAVES;
+    // K-chunk steps carrying the previous block's 16 sines, and the step that
+    // splits them: block 0 reads the chunks it produces at steps NK-2, NK-1
+    constexpr int NKS = NK >= 18 ? 16 : NK - 2;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int nh = p.nh;
+    float* wbuf = smem;                // 2 ring slots
+    float* film = smem + 2 * BLK;      // (nh+1) x H; hidden layers' rows pre-scaled by s_i
+    float* w0s = film + (nh + 1) * H;  // (H, 4)
+    float* wos = w0s + 4 * H;          // (4, H)
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5;
+    const int64_t b = p.b0 + blockIdx.y;
+    const int64_t n = (int64_t)blockIdx.x * TILE + wave * 32 + (lane & 31);
+
+    {
+        const float* fsrc = p.film + b * (int64_t)(nh + 1) * H;
+        const int nf = (nh + 1) * H;
+        for (int i = threadIdx.x * 4; i < nf; i += 64 * WAVES * 4) {
+            const int layer = i / H;
+            const float sc = layer == 0 ? 1.0f : p.wscale[layer - 1];
+            *(f4*)(film + i) = *(const f4*)(fsrc + i) * sc;  // power-of-two: exact
+        }
+    }
+    for (int f = threadIdx.x; f < H; f += 64 * WAVES) {
+        f4 w = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < p.d; ++k) w[k] = p.w0[f * p.d + k];
+        *(f4*)(w0s + 4 * f) = w;
+    }
+    for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) wos[i] = i < p.c * H ? p.wout[i] : 0.f;
+    float cn[4];
+    {
+        const int64_t nc = n < p.N ? n : p.N - 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float v = 0.f;
+            if (k < p.d) {
+                v = p.coords[nc * p.d + k];
+                if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+            }
+            cn[k] = v;
+        }
+    }
+    __syncthreads();
+    const int nblocks = nh * NB2;
+    const __amdgpu_buffer_rsrc_t wrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.wimg, 0, nblocks * (BLK * 4), 0x00020000);
+    siren_issue_block<NPC, WAVES>(p.wimg, 0, wbuf, wave, lane);
+
+    Frag BH[NK], BL[NK], NH[NK], NL[NK];
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+
+    // ---- layer 0 (d -> H, fp32 VALU): x = sin(w0 (W0 c + F_0)), into the split set ----
+    static_for<NB2>([&](auto Jc) {
+        constexpr int J = decltype(Jc)::value;
+        float x[16];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const f4 fv = *(const f4*)(film + 32 * J + 8 * qq + 4 * h);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const f4 w = *(const f4*)(w0s + 4 * (32 * J + 8 * qq + 4 * h + r));
+                float a = cn[0] * w[0];
+#pragma unroll
+                for (int k = 1; k < 4; ++k)
+                    if (k < p.d) a = fmaf(cn[k], w[k], a);
+                x[4 * qq + r] = sin1_cw(p.w0f * (a + fv[r]));
+            }
+        }
+        split_chunk(x, 0, NH[2 * J], NL[2 * J]);
+        split_chunk(x, 1, NH[2 * J + 1], NL[2 * J + 1]);
+    });
+
+    // ---- hidden layers: 3 f16 MFMAs per fp32 product ----
+    // Block j's MFMAs overlap the epilogue (sines, split or output-layer sums) of
+    // the block before it -- for j = 0 the previous layer's last block, whose
+    // chunks NK-2, NK-1 are produced at steps 16-17 and consumed at steps NK-2,
+    // NK-1 of the same block.  Block 0 reads its B operands from the VGPR split
+    // set and copies each chunk into the accumulator file for blocks 1.. (the
+    // 384 operand registers of two layers do not fit in one file).
+    static_assert(NB2 % 2 == 0, "static ring slots need an even block count");
+    int J = 0;
+    f16v prev;
+    float mprev = 0.f;
+    float x[16];
+    for (int layer = 1; layer <= nh; ++layer) {
+        const bool last = layer == nh;
+        const float m = p.w0f / p.wscale[layer - 1];  // power-of-two scale: exact
+        // output-layer partial sums over the 4 features of part e of block jp (x: its sines)
+        auto outsum = [&](int jp, int e) __attribute__((always_inline)) {  // wos rows oc >= c are zero
+            const int f = 32 * jp + 8 * e + 4 * h;
+#pragma unroll
+            for (int oc = 0; oc < 4; ++oc) {
+                const f4 w = *(const f4*)(wos + oc * H + f);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[oc] = fmaf(w[r], x[4 * e + r], o[oc]);
+            }
+        };
+        static_for<NB2>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            constexpr int jp = j == 0 ? NB2 - 1 : j - 1;  // block whose epilogue runs here
+            const float me = j == 0 ? mprev : m;
+            const bool live = j > 0 || layer > 1;        // there is such a block
+            // block J+1 into the free slot; past the last block, the last block
+            // again (branch-free; that slot is no longer read)
+            // NB2 is even, so block j of every layer uses ring slot j % 2 (static
+            // LDS offsets off one lane base)
+            float* nxt = wbuf + ((j & 1) ^ 1) * BLK;
+            const float* wb = wbuf + (j & 1) * BLK;
+            const int soff = __builtin_amdgcn_readfirstlane(min(J + 1, nblocks - 1)) * (BLK * 4);
+            f16v a;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const f4 f = *(const f4*)(film + layer * H + 32 * j + 8 * qq + 4 * h);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a[4 * qq + r] = f[r];
+            }
+            h8 FH = *(const h8*)(wb + lane * 4);
+            h8 FL = *(const h8*)(wb + 256 + lane * 4);
+            static_for<NK>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                h8 FH1 = FH, FL1 = FL;
+                if constexpr (k + 1 < NK) {
+                    FH1 = *(const h8*)(wb + (k + 1) * 512 + lane * 4);
+                    FL1 = *(const h8*)(wb + (k + 1) * 512 + 256 + lane * 4);
+                }
+                if constexpr (k < PPW && !(EXP & 1)) {
+                    const int piece = wave + WAVES * k;
+                    // buffer form: scalar base + offset, one per-lane VGPR offset (no VALU per piece)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        wrsrc, (__attribute__((address_space(3))) void*)(nxt + piece * 256), 16, lane * 16,
+                        soff + piece * 1024, 0, 0);
+                }
+                if constexpr (j == 0) {
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(FL, NH[k].h(), a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(FH, NL[k].h(), a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(FH, NH[k].h(), a, 0, 0, 0);
+                    BH[k] = NH[k];
+                    BL[k] = NL[k];
+                    asm volatile("" : "+a"(BH[k].v), "+a"(BL[k].v));
+                } else {
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(FL, BH[k].h(), a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(FH, BL[k].h(), a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(FH, BH[k].h(), a, 0, 0, 0);
+                }
+                if constexpr (k < NKS) {
+#pragma unroll
+                    for (int v = 16 * k / NKS; v < 16 * (k + 1) / NKS; ++v) {
+                        x[v] = (EXP & 2) ? prev[v] * me : sin1_cw(prev[v] * me);
+                        asm volatile("" : "+v"(x[v]));  // keep it in this step (no sinking to the split)
+                    }
+                }
+                // split (chunks 2jp, 2jp+1 of the next layer -- or, for j = 0, of this
+                // one) or, in the last layer, the output-layer sums
+                constexpr int KE = NK >= 18 ? 16 : NKS - 1;
+                if constexpr (k == KE || k == (NK >= 18 ? 17 : KE)) {
+                    constexpr bool both = NK < 18;
+                    constexpr int e0 = (NK >= 18 && k == 17) ? 1 : 0;
+                    if (live) {
+#pragma unroll
+                        for (int e = e0; e < (both ? 2 : e0 + 1); ++e)
+                            split_chunk(x, e, NH[2 * jp + e], NL[2 * jp + e]);
+                        if (j > 0 && last) {
+#pragma unroll
+                            for (int e = 2 * e0; e < (both ? 4 : 2 * e0 + 2); ++e) outsum(jp, e);
+                        }
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                FH = FH1;
+                FL = FL1;
+            });
+            prev = a;
+            // this wave's pieces of block J+1 landed; the barrier publishes every
+            // wave's pieces and retires all reads of this slot before its refill
+            // (a bare s_barrier: __syncthreads' fence would add nothing here)
+            if constexpr (!(EXP & 1)) {
+                __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+                asm volatile("s_barrier" ::: "memory");
+            }
+            ++J;
+        });
+        mprev = m;
+    }
+    // the last layer's last block
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] = sin1_cw(prev[v] * mprev);
+    {
+        const int f0 = 32 * (NB2 - 1) + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int oc = 0; oc < 4; ++oc) {
+                const f4 w = *(const f4*)(wos + oc * H + f0 + 8 * e);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[oc] = fmaf(w[r], x[4 * e + r], o[oc]);
+            }
+    }
+
+    // ---- output layer (H -> c): reduce the two lane halves, bias, de-normalise ----
+    float ov[4];
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        const float sum = o[oc] + __shfl_xor(o[oc], 32);
+        ov[oc] = oc < p.c ? sum + p.bout[oc] : 0.f;
+    }
+    if (n < p.N) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int oc = 2 * h + i;
+            if (oc < p.c) {
+                float v = ov[oc];
+                if (p.ymax) {
+                    const int64_t yi = n * p.ystride + oc;
+                    const float hi = p.ymax[yi], lo = p.ymin[yi];
+                    v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
+                }
+                p.out[(b * p.N + n) * p.c + oc] = v;
+            }
+        }
+    }
+}
+
 namespace {
 
 int env_int(const char* name, int dflt, int lo, int hi) {
@@ -360,12 +658,12 @@ int env_int(const char* name, int dflt, int lo, int hi) {
     return v >= lo && v <= hi ? v : dflt;
 }
 
-template <int NB, int RING, int CG, int RB = 1, bool NOSYNC = false>
+template <int NB, int RING, int CG, int RB = 1, bool NOSYNC = false, bool PKSIN = true>
 void launch_ring(SirenArgs a, int b, hipStream_t st) {
     constexpr int H = NB * 16;
     constexpr int WAVES = CG == 1 ? 8 : 4;
     const size_t lds = sizeof(float) * ((size_t)RING * RB * NB * 256 + (size_t)(a.nh + 1) * H + 8 * H);
-    const void* fn = (const void*)siren_fused_split<NB, WAVES, RING, CG, RB, NOSYNC>;
+    const void* fn = (const void*)siren_fused_split<NB, WAVES, RING, CG, RB, NOSYNC, PKSIN>;
     CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the split-f16 decoder's LDS staging");
     CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t tiles = ceil_div(a.N, 16 * CG * WAVES);
@@ -373,7 +671,7 @@ void launch_ring(SirenArgs a, int b, hipStream_t st) {
     for (int64_t b0 = 0; b0 < b; b0 += 65535) {
         a.b0 = b0;
         const int nb = (int)std::min<int64_t>(65535, b - b0);
-        hipLaunchKernelGGL((siren_fused_split<NB, WAVES, RING, CG, RB, NOSYNC>), dim3((unsigned)tiles, nb),
+        hipLaunchKernelGGL((siren_fused_split<NB, WAVES, RING, CG, RB, NOSYNC, PKSIN>), dim3((unsigned)tiles, nb),
                            dim3(64 * WAVES), lds, st, a);
         check_launch("siren_fused_split");
     }
@@ -389,12 +687,59 @@ void launch_nb(SirenArgs a, int b, hipStream_t st) {
         static const int nosync = env_int("CFD_SIREN_NOSYNC", 0, 0, 1);
         if (nosync) return cg == 1 ? launch_ring<NB, 2, 1, 1, true>(a, b, st) : launch_ring<NB, 2, 2, 1, true>(a, b, st);
     }
+    if constexpr (NB == 24) {  // scalar-sine variant: CFD_SIREN_PKSIN=0
+        static const int pk = env_int("CFD_SIREN_PKSIN", 1, 0, 1);
+        if (!pk && cg == 1)
+            return rb == 2 ? launch_ring<NB, 2, 1, 2, false, false>(a, b, st) : launch_ring<NB, 2, 1, 1, false, false>(a, b, st);
+    }
     // two groups of two blocks per slot when the LDS holds them, else one block per slot
     if (rb == 2 && fits2)
         return cg == 1 ? launch_ring<NB, 2, 1, 2>(a, b, st) : launch_ring<NB, 2, 2, 2>(a, b, st);
     return cg == 1 ? launch_ring<NB, 2, 1, 1>(a, b, st) : launch_ring<NB, 2, 2, 1>(a, b, st);
 }
 }  // namespace
+
+template <int NB2, int EXP = 0>
+void launch_split32(SirenArgs a, int b, hipStream_t st) {
+    constexpr int H = NB2 * 32;
+    const size_t lds = sizeof(float) * ((size_t)2 * 2 * NB2 * 512 + (size_t)(a.nh + 1) * H + 8 * H);
+    const void* fn = (const void*)siren_split32<NB2, EXP>;
+    CFD_REQUIRE((int64_t)a.nh * H * H * 4 < 0x7fffffffLL, CFD_EARG, "weight image beyond the 2 GiB buffer range");
+    CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the split-f16 decoder's LDS staging");
+    CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int64_t tiles = ceil_div(a.N, 128);
+    CFD_REQUIRE(tiles <= 0x7fffffff, CFD_EARG, "too many coordinates for one launch");
+    for (int64_t b0 = 0; b0 < b; b0 += 65535) {
+        a.b0 = b0;
+        const int nb = (int)std::min<int64_t>(65535, b - b0);
+        hipLaunchKernelGGL((siren_split32<NB2, EXP>), dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
+        check_launch("siren_split32");
+    }
+}
+
+bool siren_split32_supported(int H, int nh) {
+    const size_t film = (size_t)(nh + 1) * H + 8 * (size_t)H;
+    return (H == 64 || H == 128 || H == 256 || H == 384) &&
+           sizeof(float) * ((size_t)4 * (H / 32) * 512 + film) <= 160 * 1024;
+}
+
+void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
+    switch (H) {
+        case 64: return launch_split32<2>(a, b, st);
+        case 128: return launch_split32<4>(a, b, st);
+        case 256: return launch_split32<8>(a, b, st);
+        case 384: {
+            static const int exp = env_int("CFD_SIREN_EXP", 0, 0, 3);
+            switch (exp) {
+                case 1: return launch_split32<12, 1>(a, b, st);
+                case 2: return launch_split32<12, 2>(a, b, st);
+                case 3: return launch_split32<12, 3>(a, b, st);
+                default: return launch_split32<12>(a, b, st);
+            }
+        }
+        default: throw Error{CFD_EARG, "32x32 split-f16 SIREN needs hidden_features in {64, 128, 256, 384}"};
+    }
+}
 
 bool siren_split_supported(int NB) {
     switch (NB) {
