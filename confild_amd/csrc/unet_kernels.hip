@@ -144,6 +144,175 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
     *(f4*)(a.out + pix * a.Ctot + c0) = v;
 }
 
+// K3f: the same GroupNorm(+SiLU) in ONE launch: workgroup = (sample, group).
+// Pass 1 sums the group's HW x cpg elements (thread t: channel quad t % nq of
+// every (256/nq)-th pixel, float64), a fixed-order tree gives mean / rstd; pass
+// 2 re-reads the same elements (L2-resident: the 32 groups of one sample run on
+// one XCD, see the block mapping) and writes y = x*scale + shift (+ SiLU).
+// Same statistics, affine form and output as the three-kernel path, one launch
+// instead of three (the path is latency-bound at these sizes); batch-invariant
+// (a sample's summation order does not depend on B).
+__global__ __launch_bounds__(256) void gn_fused_kernel(GnArgs a) {
+    // linear block L -> (b = L % B, grp = L / B): consecutive L go round-robin over
+    // the 8 XCDs, so with B % 8 == 0 every group of sample b shares one L2
+    const int L = blockIdx.x;
+    const int64_t b = L % a.B;
+    const int grp = L / a.B;
+    const int Ctot = a.Ctot, cpg = Ctot / 32, nq = cpg / 4;
+    const int HW = a.HW;
+    const int rows = 256 / nq;  // pixels per sweep
+    const int t = threadIdx.x;
+    const bool act = t < rows * nq;
+    const int q = t % nq, r0 = t / nq;
+    const int c = grp * cpg + 4 * q;
+    const float* src = c < a.C1 ? a.src1 + b * HW * a.C1 + c : a.src2 + b * HW * a.C2 + (c - a.C1);
+    const int ld = c < a.C1 ? a.C1 : a.C2;
+    __shared__ double red[2][256];
+    __shared__ float sh[2][32];
+    double s = 0, s2 = 0;
+    if (act) {
+        for (int p = r0; p < HW; p += rows) {
+            const f4 v = *(const f4*)(src + (int64_t)p * ld);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s += v[j];
+                s2 += (double)v[j] * v[j];
+            }
+        }
+    }
+    red[0][t] = s;
+    red[1][t] = s2;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {  // fixed-order tree
+        if (t < w) {
+            red[0][t] += red[0][t + w];
+            red[1][t] += red[1][t + w];
+        }
+        __syncthreads();
+    }
+    if (t < cpg) {
+        const double n = (double)HW * cpg;
+        const double mean = red[0][0] / n;
+        const double var = fmax(red[1][0] / n - mean * mean, 0.0);
+        const float mf = (float)mean, rf = (float)(1.0 / sqrt(var + (double)a.eps));
+        const int cc = grp * cpg + t;
+        const float sc = rf * a.gamma[cc];
+        const float sf = a.beta[cc] - mf * sc;
+        sh[0][t] = sc;
+        sh[1][t] = sf;
+        a.ss[(b * Ctot + cc) * 2 + 0] = sc;
+        a.ss[(b * Ctot + cc) * 2 + 1] = sf;
+        if (a.stats && t == 0) {
+            a.stats[(b * 32 + grp) * 2 + 0] = mf;
+            a.stats[(b * 32 + grp) * 2 + 1] = rf;
+        }
+    }
+    __syncthreads();
+    if (!act) return;
+    f4 sc, sf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        sc[j] = sh[0][4 * q + j];
+        sf[j] = sh[1][4 * q + j];
+    }
+    float* dst = a.out + b * HW * Ctot + c;
+    for (int p = r0; p < HW; p += rows) {
+        f4 v = *(const f4*)(src + (int64_t)p * ld);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = v[j] * sc[j] + sf[j];
+            if (a.silu) v[j] = silu_f(v[j]);
+        }
+        *(f4*)(dst + (int64_t)p * Ctot) = v;
+    }
+}
+
+// Register-resident form for HW x cpg <= 512 x IPT x 4: 512 threads, each
+// loading its IPT float4 at once (the loads pipeline instead of forming a
+// latency chain), summing them, and normalising the same registers (one HBM
+// read instead of two).  Same statistics / order semantics as gn_fused_kernel.
+template <int IPT>
+__global__ __launch_bounds__(512) void gn_fused_reg_kernel(GnArgs a) {
+    constexpr int NT = 512;
+    const int L = blockIdx.x;
+    const int64_t b = L % a.B;
+    const int grp = L / a.B;
+    const int Ctot = a.Ctot, cpg = Ctot / 32, nq = cpg / 4;
+    const int HW = a.HW;
+    const int rows = NT / nq;
+    const int t = threadIdx.x;
+    const bool act = t < rows * nq;
+    const int q = t % nq, r0 = t / nq;
+    const int c = grp * cpg + 4 * q;
+    const float* src = c < a.C1 ? a.src1 + b * HW * a.C1 + c : a.src2 + b * HW * a.C2 + (c - a.C1);
+    const int ld = c < a.C1 ? a.C1 : a.C2;
+    __shared__ double red[2][NT];
+    __shared__ float sh[2][32];
+    f4 v[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const int p = r0 + k * rows;
+        v[k] = act && p < HW ? *(const f4*)(src + (int64_t)p * ld) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    double s = 0, s2 = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            s += v[k][j];
+            s2 += (double)v[k][j] * v[k][j];
+        }
+    red[0][t] = s;
+    red[1][t] = s2;
+    __syncthreads();
+    for (int w = NT / 2; w > 0; w >>= 1) {  // fixed-order tree
+        if (t < w) {
+            red[0][t] += red[0][t + w];
+            red[1][t] += red[1][t + w];
+        }
+        __syncthreads();
+    }
+    if (t < cpg) {
+        const double n = (double)HW * cpg;
+        const double mean = red[0][0] / n;
+        const double var = fmax(red[1][0] / n - mean * mean, 0.0);
+        const float mf = (float)mean, rf = (float)(1.0 / sqrt(var + (double)a.eps));
+        const int cc = grp * cpg + t;
+        const float sc = rf * a.gamma[cc];
+        const float sf = a.beta[cc] - mf * sc;
+        sh[0][t] = sc;
+        sh[1][t] = sf;
+        a.ss[(b * Ctot + cc) * 2 + 0] = sc;
+        a.ss[(b * Ctot + cc) * 2 + 1] = sf;
+        if (a.stats && t == 0) {
+            a.stats[(b * 32 + grp) * 2 + 0] = mf;
+            a.stats[(b * 32 + grp) * 2 + 1] = rf;
+        }
+    }
+    __syncthreads();
+    if (!act) return;
+    f4 sc, sf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        sc[j] = sh[0][4 * q + j];
+        sf[j] = sh[1][4 * q + j];
+    }
+    float* dst = a.out + b * HW * Ctot + c;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const int p = r0 + k * rows;
+        if (p < HW) {
+            f4 y;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                y[j] = v[k][j] * sc[j] + sf[j];
+                if (a.silu) y[j] = silu_f(y[j]);
+            }
+            *(f4*)(dst + (int64_t)p * Ctot) = y;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K1/K2: implicit-GEMM convolution.  GEMM view: M = B*Hout*Wout output pixels,
 // N = Cout, K = ks*ks*Ctot ordered (tap, channel).  Workgroup tile BM x BN x 32,
@@ -659,12 +828,35 @@ __global__ void linear_kernel(const float* __restrict__ x, const float* __restri
 // ---------------------------------------------------------------------------
 int gn_chunks(int HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 16)); }
 
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     CFD_REQUIRE(a0.Ctot % 32 == 0 && a0.C1 % 4 == 0 && a0.C2 % 4 == 0 && a0.Ctot <= 1024, CFD_ESHAPE,
                 "GroupNorm32 needs channels % 32 == 0 (<= 1024)");
     GnArgs a = a0;
     a.nchunks = gn_chunks(a.HW);
     a.B = B;
+    static const int fused = env_int("CFD_GN_FUSED", 1);
+    if (fused && a.Ctot % 128 == 0) {
+        const int nq = a.Ctot / 128, rows = 512 / nq;
+        const int ipt = (int)ceil_div(a.HW, rows);
+        const dim3 grid((unsigned)(32 * B));
+        if (fused == 2 || ipt > 32)
+            hipLaunchKernelGGL(gn_fused_kernel, grid, dim3(256), 0, st, a);
+        else if (ipt <= 4)
+            hipLaunchKernelGGL(gn_fused_reg_kernel<4>, grid, dim3(512), 0, st, a);
+        else if (ipt <= 8)
+            hipLaunchKernelGGL(gn_fused_reg_kernel<8>, grid, dim3(512), 0, st, a);
+        else if (ipt <= 16)
+            hipLaunchKernelGGL(gn_fused_reg_kernel<16>, grid, dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL(gn_fused_reg_kernel<32>, grid, dim3(512), 0, st, a);
+        check_launch("gn_fused_kernel");
+        return;
+    }
     hipLaunchKernelGGL(gn_partial_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
     check_launch("gn_partial_kernel");
     hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(256), 0, st, a);
@@ -674,10 +866,6 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     check_launch("gn_apply_kernel");
 }
 
-static int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
 
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // Every choice is made from the per-sample shape (as if the batch were 8),
