@@ -346,13 +346,17 @@ __device__ __forceinline__ int lds_swz_bf(int row, int chunk) { return row * 64 
 // accumulate): 22-bit operands, exact products, the fp32 accumulation order of
 // the fp32 kernel -- error against fp64 at the fp32 kernel's level
 // (tests/test_gpu_unet_split.py).  hi and lo tiles use the bf16 LDS layout.
-template <int BM, int BN, bool TMODE, int MODE>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
+// NW waves as (NW/2) x 2; 8 waves with BM = 128 halve the weight-tile reads per
+// output pixel at the same per-wave tile.
+template <int BM, int BN, bool TMODE, int MODE, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(ConvArgs a) {
     constexpr bool BF = MODE == 1, SP = MODE == 2;
     constexpr int BK = 32;
-    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int WM = BM / (NW / 2), WN = BN / 2;
     constexpr int TM = WM / 16, TN = WN / 16;
-    constexpr int AIT = BM / 32, BIT = BN / 32;  // float4 (bf16: 4 x bf16) per thread per tile
+    constexpr int RPP = 8 * NW;                  // staged rows per pass (8 threads per 32-deep row)
+    constexpr int AIT = BM / RPP, BIT = BN / RPP;  // float4 (bf16: 4 x bf16) per thread per tile
+    static_assert(AIT >= 1 && BIT >= 1 && TM >= 1, "tile too small for the wave count");
     // floats per LDS tile: fp32 BM*BK; bf16 half that; split two f16 tiles (hi, lo)
     constexpr int AFL = BF ? BM * BK / 2 : BM * BK, BFL = BF ? BN * BK / 2 : BN * BK;
     __shared__ __attribute__((aligned(16))) float As[2][AFL];
@@ -368,7 +372,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     bool a_ok[AIT];
 #pragma unroll
     for (int it = 0; it < AIT; ++it) {
-        const int m = m0 + rsub + it * 32;
+        const int m = m0 + rsub + it * RPP;
         a_ok[it] = m < a.M;
         const int mm = a_ok[it] ? m : 0;
         a_b[it] = mm / HWo;
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     bool b_ok[BIT];
 #pragma unroll
     for (int it = 0; it < BIT; ++it) {
-        const int n = n0 + rsub + it * 32;
+        const int n = n0 + rsub + it * RPP;
         b_ok[it] = n < a.Cout;
         if constexpr (BF || SP)
             wrow_bf[it] = (const unsigned short*)a.wbf + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
@@ -474,13 +478,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
             for (int it = 0; it < AIT; ++it) {
                 const h4 hv = __builtin_convertvector(ra[it], h4);
                 const h4 lv = __builtin_convertvector(ra[it] - __builtin_convertvector(hv, f4), h4);
-                const int off = lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8;
+                const int off = lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8;
                 *(h4*)((char*)As[buf] + off) = hv;
                 *(h4*)((char*)As[buf] + BM * BK * 2 + off) = lv;
             }
 #pragma unroll
             for (int it = 0; it < BIT; ++it) {
-                const int off = lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8;
+                const int off = lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8;
                 *(uint2*)((char*)Bs[buf] + off) = rbh[it];
                 *(uint2*)((char*)Bs[buf] + BN * BK * 2 + off) = rbl[it];
             }
@@ -489,16 +493,16 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
             for (int it = 0; it < AIT; ++it) {
                 const bf16x4 v = __builtin_convertvector(ra[it], bf16x4);
-                *(bf16x4*)((char*)As[buf] + lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8) = v;
+                *(bf16x4*)((char*)As[buf] + lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8) = v;
             }
 #pragma unroll
             for (int it = 0; it < BIT; ++it)
-                *(uint2*)((char*)Bs[buf] + lds_swz_bf(rsub + it * 32, kq >> 1) + (kq & 1) * 8) = rbh[it];
+                *(uint2*)((char*)Bs[buf] + lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8) = rbh[it];
         } else {
 #pragma unroll
-            for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][lds_swz(rsub + it * 32, kq)]) = ra[it];
+            for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][lds_swz(rsub + it * RPP, kq)]) = ra[it];
 #pragma unroll
-            for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][lds_swz(rsub + it * 32, kq)]) = rb[it];
+            for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][lds_swz(rsub + it * RPP, kq)]) = rb[it];
         }
     };
 
@@ -874,15 +878,26 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // (or rank shard) it is computed in.  Knobs (development): CFD_CONV_BM
     // (0 = auto), CFD_CONV_TARGET_WG.
     static const int force_bm = env_int("CFD_CONV_BM", 0);
-    static const int target = env_int("CFD_CONV_TARGET_WG", 512);
+    static const int target = env_int("CFD_CONV_TARGET_WG", 1024);
     ConvPlan p;
     const int64_t mn = (int64_t)8 * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;
     auto tiles = [&](int bm) { return ceil_div(mn, bm) * ceil_div(a.Cout, p.bn); };
     p.bm = force_bm ? force_bm : 64;  // 64x128 measured ahead of 128x128 (r01 sweep: 8.76 vs 9.26 ms)
+    // 8-wave 128x128 tiles for Cout >= 128 (CFD_CONV_NW8: 2 = everywhere, 1 = where
+    // they fill the chip without split-K, 0 = never), counted as 2 WGs each.
+    // Measured B=8 64^2 forward: 5.88 ms (0), 5.69 (1), 5.51 (2, 1024-WG target).
+    static const int nw8 = env_int("CFD_CONV_NW8", 2);
+    int wg_per_tile = 1;
+    if (!force_bm && p.bn == 128 && (nw8 == 2 || (nw8 == 1 && tiles(128) >= 256))) {
+        p.bm = 128;
+        p.nw = 8;
+        wg_per_tile = 2;
+    }
     const int nkt = a.K / 32;
     p.splits = 1;
-    while (tiles(p.bm) * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16) p.splits *= 2;
+    while (tiles(p.bm) * wg_per_tile * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16)
+        p.splits *= 2;
     // memory guard, on the nominal shape too: part_cap_floats is the slab per 8
     // samples (the caller sizes the real slab as ceil(B/8) of these)
     while (p.splits > 1 && (size_t)p.splits * mn * a.Cout > part_cap_floats) p.splits /= 2;
@@ -891,7 +906,9 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
 
 template <bool TMODE, int MODE>
 static void launch_conv_tiles(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-    if (p.bm == 128 && p.bn == 128)
+    if (p.nw == 8 && p.bm == 128 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE, 8>), grid, dim3(512), 0, st, a);
+    else if (p.bm == 128 && p.bn == 128)
         hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE>), grid, dim3(256), 0, st, a);
     else if (p.bm == 64 && p.bn == 128)
         hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE, MODE>), grid, dim3(256), 0, st, a);

@@ -82,6 +82,7 @@ struct AttnBwdArgs {
 
 struct ConvPlan {
     int bm = 128, bn = 128, splits = 1;
+    int nw = 4;  // waves per workgroup (8: BM = BN = 128 only)
 };
 
 int gn_chunks(int HW);
