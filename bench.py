@@ -49,8 +49,8 @@ HBM_PEAK_GBS = 8000.0
 # dominant-kernel roofline per decoder compute mode:
 #   (kernel name, peak in algorithmic fp32 TFLOP/s, basis, committed PMC record)
 ROOFLINE = {
-    "split_f16": ("siren_fused_split", F16_PEAK_TFLOPS / 3,
-                  "f16 dense MFMA peak / 3 (three f16 MFMAs per fp32 product)", "r01_siren_split_pmc.json"),
+    "split_f16": ("siren_split32", F16_PEAK_TFLOPS / 3,
+                  "f16 dense MFMA peak / 3 (three f16 MFMAs per fp32 product)", "r01_siren_split32_pmc.json"),
     "f32": ("siren_fused", FMA_PEAK_TFLOPS, "fp32 MFMA peak", "r01_siren_pmc.json"),
 }
 
@@ -244,8 +244,8 @@ def main():
             "compute": {"unet": ("fp32 via split-f16 convolutions (3x v_mfma_f32_16x16x32_f16 on 22-bit operand "
                                  "splits; error vs fp64 = fp32's, DESIGN.md K1s); GroupNorm/softmax/attention fp32"
                                  if objs[0].compute == "split_f16" else "fp32 (v_mfma_f32_16x16x4_f32)"),
-                        "cnf_decoder": ("fp32 via split-f16 (3x v_mfma_f32_16x16x32_f16 on 22-bit operand "
-                                        "splits; error vs fp64 = fp32's, DESIGN.md K7s)" if mode == "split_f16"
+                        "cnf_decoder": ("fp32 via split-f16 (3x v_mfma_f32_32x32x16_f16 on 22-bit operand "
+                                        "splits; error vs fp64 = fp32's, DESIGN.md K7t)" if mode == "split_f16"
                                         else "fp32 (v_mfma_f32_16x16x4_f32)")},
             "config": {"workload": "Case4 uncond: U-Net 64x64 B=8/GPU, DDPM 256 steps (cosine, respaced), "
                                    "CNF SIREN(3,64,3,15,384) decode of 8x64 latents on a 64^3 lattice",

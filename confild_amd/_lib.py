@@ -11,6 +11,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libconfild_hip.so")
+# development A/B runs only: CFD_LIB names another in-tree build of the same library
+if os.environ.get("CFD_LIB"):
+    LIB_PATH = os.path.join(_HERE, "lib", os.path.basename(os.environ["CFD_LIB"]))
 
 _lock = threading.Lock()
 _lib = None

@@ -11,5 +11,5 @@ S=$(find gpurun_out/prof_bench -name "*kernel_stats.csv" | head -1); cp $S gpuru
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- python3 tools/kbench.py siren --latents 512 > gpurun_out/pmc_f.log 2>&1 || { tail -5 gpurun_out/pmc_f.log; exit 11; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w -o run -- python3 tools/kbench.py siren --latents 512 > gpurun_out/pmc_w.log 2>&1 || { tail -5 gpurun_out/pmc_w.log; exit 12; }
 F=$(find gpurun_out/pmc_f -name "*counter_collection.csv" | head -1); W=$(find gpurun_out/pmc_w -name "*counter_collection.csv" | head -1)
-python3 tools/pmc_traffic.py $F $W "siren_fused_split<" gpurun_out/profiles_new/r01_siren_split_pmc.json 1628980992 '{"latents": 512, "coords": 262144, "dims": [3, 64, 3, 15, 384]}' || exit 13
+python3 tools/pmc_traffic.py $F $W "siren_split32<" gpurun_out/profiles_new/r01_siren_split32_pmc.json 1628980992 '{"latents": 512, "coords": 262144, "dims": [3, 64, 3, 15, 384]}' || exit 13
 echo done

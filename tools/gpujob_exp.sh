@@ -6,7 +6,4 @@ timeout -k 10 200 python tools/kbench.py unet --unet-compute split_f16 > gpurun_
 grep kernel gpurun_out/kb_u.log
 timeout -k 10 200 python tools/kbench.py unet --unet-compute fp32 > gpurun_out/kb_u.log 2>&1 || { cat gpurun_out/kb_u.log; exit 2; }
 grep kernel gpurun_out/kb_u.log
-timeout -k 10 200 python tools/kbench.py dps > gpurun_out/kb_d.log 2>&1 || { cat gpurun_out/kb_d.log; exit 2; }
-grep kernel gpurun_out/kb_d.log
-CFD_CONV_NW8=0 CFD_CONV_TARGET_WG=512 timeout -k 10 200 python tools/kbench.py dps > gpurun_out/kb_d.log 2>&1 || { cat gpurun_out/kb_d.log; exit 2; }
-grep kernel gpurun_out/kb_d.log
+bash tools/gpujob_pmc_unet.sh
