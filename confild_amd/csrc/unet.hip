@@ -295,6 +295,7 @@ struct Tape {
 
 struct Sizes {
     size_t max_act = 0, max_qkv = 0, max_cat = 0, max_att = 0;  // floats per sample
+    size_t max_kvf = 0;  // split attention's packed K/V fragments (any level)
     std::vector<size_t> hs;                                     // skip-stack tensors, floats per sample
 };
 
@@ -313,6 +314,7 @@ Sizes sizes(const cfd_unet* h) {
         // normalised concat input of an output block: hw^2 * (C_level + C_max)
         z.max_cat = std::max(z.max_cat, (size_t)hw * hw * (co + cmax));
         z.max_att = std::max(z.max_att, (size_t)hw * hw * co);  // heads * T <= C * T
+        z.max_kvf = std::max(z.max_kvf, cfd::attention_split_floats(hw * hw, co));
         for (int r = 0; r < c.num_res_blocks; ++r) z.hs.push_back((size_t)hw * hw * co);
         ch = co;
         if (l != c.n_mult - 1) {
@@ -355,6 +357,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     // normalised (+SiLU) input of the next conv (widest: an output block's concat)
     float* nbuf = ws.take((size_t)B * z.max_cat);
     float* splitk = ws.take(kSplitCap);
+    float* kvws = ws.take((size_t)B * z.max_kvf);
     float* pool[3];
     for (auto& p : pool) p = ws.take((size_t)B * z.max_act);
     float* tmp = ws.take((size_t)B * z.max_act);
@@ -534,7 +537,12 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 rec.qkv = qb;
                 rec.o = ob;
                 rec.lse = aa.lse;
-                if (launch) cfd::launch_attention(aa, at.ch, at.heads, B, st);
+                if (launch) {
+                    if (h->compute == CFD_COMPUTE_SPLIT_F16 && (at.ch == 32 || at.ch == 64 || at.ch == 128))
+                        cfd::launch_attention_split(aa, at.ch, at.heads, B, kvws, st);
+                    else
+                        cfd::launch_attention(aa, at.ch, at.heads, B, st);
+                }
                 float* out = dest(cur.a, nullptr, (size_t)B * T * at.C);
                 conv(Act{ob, at.C, nullptr, 0, cur.H, cur.W}, at.pre + ".proj_out", at.C, 1, 1, 0, nullptr, cur.a,
                      out);

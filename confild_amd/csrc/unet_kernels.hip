@@ -790,6 +790,177 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// K4s: the same attention at fp32 accuracy on f16 MFMA (split compute).
+// attn_kv_split packs K (times the q/k scale) and V once per call as hi/lo f16
+// MFMA fragments (x = hi + lo, 22 significant bits), keys padded to a multiple
+// of 32 with zeros:
+//   Kf[b][h][kt][j][hl][lane][8]: key 16 kt + lane%16, channel 32 j + 8(lane/16) + t
+//   Vf[b][h][kb][dd][hl][lane][8]: channel 16 dd + lane%16, key 32 kb + kmap(lane/16, t)
+// with kmap(g, t) = 4g + t (t < 4), 16 + 4g + t - 4 (t >= 4): the keys a lane holds
+// of two 16-key S^T tiles, so P^T feeds the P.V MFMA straight from the softmax
+// registers.  attention_split_kernel then runs S^T = K Q^T and O^T = V^T P^T as
+// three v_mfma_f32_16x16x32_f16 each (lo*hi + hi*lo + hi*hi, fp32 accumulate) over
+// 32-key blocks with the fp32 kernel's online softmax.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void split8_f16(const float (&v)[8], h8v& hi, h8v& lo) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        hi[t] = (_Float16)v[t];
+        lo[t] = (_Float16)(v[t] - (float)hi[t]);
+    }
+}
+
+__global__ __launch_bounds__(256) void attn_kv_split_kernel(AttnArgs a, int CH, int heads, int B, h8v* kf,
+                                                            h8v* vf) {
+    const int T = a.T, T32 = (T + 31) / 32 * 32;
+    const int nj = CH / 32, nd = CH / 16;
+    // slots: K (T32/16 * nj * 64) then V (T32/32 * nd * 64) per (b, h)
+    const int64_t kslots = (int64_t)(T32 / 16) * nj * 64, vslots = (int64_t)(T32 / 32) * nd * 64;
+    const int64_t per = kslots + vslots;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per * heads * B) return;
+    const int64_t bh = i / per;
+    int64_t r = i - bh * per;
+    const int64_t b = bh / heads;
+    const int h = (int)(bh - b * heads);
+    const int C3 = 3 * a.C;
+    const float* base = a.qkv + b * (int64_t)T * C3 + (int64_t)h * 3 * CH;
+    const int lane = (int)(r & 63), g = lane >> 4, li = lane & 15;
+    float v[8];
+    h8v* dst;
+    int64_t stride;
+    if (r < kslots) {
+        const int64_t f = r >> 6;  // fragment (kt, j)
+        const int kt = (int)(f / nj), j = (int)(f - (int64_t)kt * nj);
+        const int key = 16 * kt + li;
+        const float* kp = base + (int64_t)min(key, T - 1) * C3 + CH + 32 * j + 8 * g;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = key < T ? kp[t] * a.scale : 0.f;
+        dst = kf + ((bh * (T32 / 16) + kt) * nj + j) * 128 + lane;
+        stride = 64;
+    } else {
+        r -= kslots;
+        const int64_t f = r >> 6;  // fragment (kb, dd)
+        const int kb = (int)(f / nd), dd = (int)(f - (int64_t)kb * nd);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int key = 32 * kb + (t < 4 ? 4 * g + t : 16 + 4 * g + t - 4);
+            v[t] = key < T ? base[(int64_t)key * C3 + 2 * CH + 16 * dd + li] : 0.f;
+        }
+        dst = vf + ((bh * (T32 / 32) + kb) * nd + dd) * 128 + lane;
+        stride = 64;
+    }
+    h8v hi, lo;
+    split8_f16(v, hi, lo);
+    dst[0] = hi;
+    dst[stride] = lo;
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const h8v* __restrict__ kf,
+                                                              const h8v* __restrict__ vf) {
+    constexpr int NJ = CH / 32;  // 32-deep k-chunks of the head dimension
+    constexpr int ND = CH / 16;  // 16-wide output blocks
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, li = lane & 15;
+    const int h = blockIdx.y, heads = gridDim.y;
+    const int64_t b = blockIdx.z;
+    const int T = a.T, T32 = (T + 31) / 32 * 32;
+    const int q0 = blockIdx.x * 64 + wave * 16;
+    if (q0 >= T) return;  // wave-uniform
+    const int C3 = 3 * a.C;
+    const float* base = a.qkv + b * (int64_t)T * C3 + (int64_t)h * 3 * CH;
+    const int64_t bh = b * heads + h;
+    const h8v* kfb = kf + bh * (T32 / 16) * NJ * 128 + lane;
+    const h8v* vfb = vf + bh * (T32 / 32) * ND * 128 + lane;
+
+    h8v qh[NJ], ql[NJ];
+    {
+        const int tq = min(q0 + li, T - 1);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const float* qp = base + (int64_t)tq * C3 + 32 * j + 8 * g;
+            float v[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] = qp[t] * a.scale;
+            split8_f16(v, qh[j], ql[j]);
+        }
+    }
+    f4 O[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) O[d] = f4{0.f, 0.f, 0.f, 0.f};
+    float mrun = -INFINITY, lrun = 0.f;
+
+    for (int kb = 0; kb < T32; kb += 32) {
+        // S^T[key][query] of two 16-key tiles
+        f4 st[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            st[u] = f4{0.f, 0.f, 0.f, 0.f};
+            const h8v* kp = kfb + (int64_t)((kb >> 4) + u) * NJ * 128;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const h8v kh = kp[j * 128], kl = kp[j * 128 + 64];
+                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qh[j], st[u], 0, 0, 0);
+                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, ql[j], st[u], 0, 0, 0);
+                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[j], st[u], 0, 0, 0);
+            }
+        }
+        // lane (g, li) holds S[query li][key kb + 16u + 4g + r]
+        float mx = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (kb + 16 * u + 4 * g + r >= T) st[u][r] = -INFINITY;
+                mx = fmaxf(mx, st[u][r]);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(mrun, mx);
+        const float alpha = expf(mrun - mnew);
+        float p[8], ps = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                p[4 * u + r] = expf(st[u][r] - mnew);
+                ps += p[4 * u + r];
+            }
+        ps += __shfl_xor(ps, 16);
+        ps += __shfl_xor(ps, 32);
+        lrun = lrun * alpha + ps;
+        mrun = mnew;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) O[d] = O[d] * alpha;
+        // O^T[d][query] += V^T[d][key] P^T[key][query]; element t of this lane's
+        // P^T operand is key kmap(g, t) = p[t]
+        h8v ph, pl;
+        split8_f16(p, ph, pl);
+        const h8v* vp = vfb + (int64_t)(kb >> 5) * ND * 128;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            const h8v vh = vp[d * 128], vl = vp[d * 128 + 64];
+            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, O[d], 0, 0, 0);
+            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, O[d], 0, 0, 0);
+            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, O[d], 0, 0, 0);
+        }
+    }
+    // lane (g, li) holds O[query li][16 d + 4 g + r]
+    const int tq = q0 + li;
+    if (a.lse && g == 0 && tq < T) a.lse[((int64_t)b * gridDim.y + h) * T + tq] = mrun + logf(lrun);
+    if (tq < T) {
+        float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
+        const float inv = 1.0f / lrun;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            f4 v = O[d] * inv;
+            *(f4*)(op + 16 * d + 4 * g) = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K5: timestep embedding and small dense layers.
 // ---------------------------------------------------------------------------
 __global__ void temb_kernel(const int64_t* __restrict__ t, const float* __restrict__ freqs, float* __restrict__ out,
@@ -963,6 +1134,27 @@ void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t s
         default: throw Error{CFD_ESHAPE, "attention head channels must be 16, 32, 64 or 128"};
     }
     check_launch("attention_kernel");
+}
+
+size_t attention_split_floats(int T, int C) { return (size_t)(T + 31) / 32 * 32 * C * 2; }
+
+void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st) {
+    CFD_REQUIRE(CH == 32 || CH == 64 || CH == 128, CFD_ESHAPE, "split attention needs head channels 32, 64 or 128");
+    const int T32 = (a.T + 31) / 32 * 32;
+    h8v* kf = (h8v*)kvws;
+    h8v* vf = kf + (size_t)B * heads * (T32 / 16) * (CH / 32) * 128;
+    const int64_t slots = (int64_t)B * heads * ((T32 / 16) * (CH / 32) * 64 + (T32 / 32) * (CH / 16) * 64);
+    hipLaunchKernelGGL(attn_kv_split_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, st, a, CH, heads, B,
+                       kf, vf);
+    check_launch("attn_kv_split_kernel");
+    const dim3 grid((unsigned)ceil_div(a.T, 64), heads, B);
+    switch (CH) {
+        case 32: hipLaunchKernelGGL(attention_split_kernel<32>, grid, dim3(256), 0, st, a, kf, vf); break;
+        case 64: hipLaunchKernelGGL(attention_split_kernel<64>, grid, dim3(256), 0, st, a, kf, vf); break;
+        case 128: hipLaunchKernelGGL(attention_split_kernel<128>, grid, dim3(256), 0, st, a, kf, vf); break;
+        default: throw Error{CFD_ESHAPE, "split attention head channels must be 32, 64 or 128"};
+    }
+    check_launch("attention_split_kernel");
 }
 
 void launch_temb(const int64_t* t, const float* freqs, float* out, int dim, int B, hipStream_t st) {

@@ -95,6 +95,9 @@ void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st);
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
 void launch_conv_out(const ConvArgs& a, hipStream_t st);
 void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t st);
+// split-f16 attention (K4s); kvws holds attention_split_floats(T, C) floats per sample
+size_t attention_split_floats(int T, int C);
+void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st);
 // backward (unet_vjp.hip)
 void launch_gn_bwd(const GnbArgs& a, int B, hipStream_t st);
 void launch_attention_bwd(const AttnBwdArgs& a, int CH, int heads, int B, hipStream_t st);
