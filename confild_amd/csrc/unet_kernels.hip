@@ -334,9 +334,16 @@ __device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 32 + 4
 // BF (config E): bf16 operands, fp32 accumulate on v_mfma_f32_16x16x32_bf16.  The
 // fp32 activations are rounded to bf16 (RNE, v_cvt_pk_bf16_f32) as the A tile is
 // staged; weights come pre-rounded (a.wbf).  An LDS row is 32 bf16 = four 16-B
-// chunks, chunk c of row r stored at ((c + (r>>2)) & 3): one ds_read_b128 per lane
-// (k = 8g..8g+7, the MFMA operand layout), conflict-free.
-__device__ __forceinline__ int lds_swz_bf(int row, int chunk) { return row * 64 + ((chunk + (row >> 2)) & 3) * 16; }
+// chunks, chunk c of row r stored in slot (c + 2 * ((r >> 2) & 1)) & 3: one
+// ds_read_b128 per lane (k = 8g..8g+7, the MFMA operand layout), conflict-free.
+// Chunk slot (chunk + 2 * bit 2 of the row) & 3: each of ds_read_b128's four
+// 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32; rows li, chunk
+// lane/16) then covers all 64 banks once (the earlier (chunk + row/4) & 3 put
+// two lanes of every group on one 16-byte slot: 37% extra LDS cycles measured),
+// and a ds_write_b64 pair of rows fills 128 contiguous bytes.
+__device__ __forceinline__ int lds_swz_bf(int row, int chunk) {
+    return row * 64 + ((chunk + 2 * ((row >> 2) & 1)) & 3) * 16;
+}
 
 // SPLIT (MODE 2, default fp32 path): fp32-accurate convolution on f16 MFMA.
 // Activations are split as staged, x = xh + xl (xh = f16(x), xl = f16(x - xh),

@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_unet_split.py -x -q --timeout 200 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/ab_tests.log; exit 1; }
 tail -1 gpurun_out/ab_tests.log
 for r in 1 2 3; do
-for L in libconfild_hip.so libconfild_hip_old.so; do
-CFD_LIB=$L timeout -k 10 200 python tools/kbench.py unet --unet-compute split_f16 > gpurun_out/kb_u.log 2>&1 || { cat gpurun_out/kb_u.log; exit 2; }
-echo "$L $(grep kernel gpurun_out/kb_u.log | cut -c60-200)"
+for V in "CFD_LIB=libconfild_hip.so" "CFD_LIB=libconfild_hip_old.so" ${AB_EXTRA}; do
+env $V timeout -k 10 200 python tools/kbench.py unet --unet-compute split_f16 > gpurun_out/kb_u.log 2>&1 || { cat gpurun_out/kb_u.log; exit 2; }
+echo "$V $(grep kernel gpurun_out/kb_u.log | cut -c60-200)"
 done; done
