@@ -388,6 +388,19 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, st);
     }
 
+    // A split-K convolution's reduction is deferred to its consumer: the
+    // GroupNorm that reads it (GnArgs::kpart) or, before any other launch,
+    // splitk_reduce (flush).  The partial slab is shared, so a convolution
+    // also flushes first.
+    struct Pending {
+        cfd::ConvArgs a{};
+        int splits = 0;
+    } pend;
+    auto flush = [&]() {
+        if (pend.splits > 1 && launch) cfd::launch_splitk_reduce(pend.a, pend.splits, st);
+        pend.splits = 0;
+    };
+
     // GroupNorm(+SiLU) of `in` materialised once into nbuf (contiguous Ctot channels);
     // with a tape the scale/shift and group statistics are kept in *ss / *stats
     auto gn = [&](const Act& in, const std::string& pre, int silu, float** ss, float** stats) -> Act {
@@ -409,6 +422,18 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         g.HW = in.H * in.W;
         g.eps = 1e-5f;
         g.silu = silu;
+        if (pend.splits > 1 && pend.a.out == in.a && pend.a.Cout == in.Ca && cfd::gn_takes_splitk(g, B)) {
+            g.kpart = pend.a.part;
+            g.ksplits = pend.splits;
+            g.kbias = pend.a.bias;
+            g.kemb = pend.a.emb;
+            g.kemb_stride = pend.a.emb_stride;
+            g.kres = pend.a.res;
+            g.kx = pend.a.out;
+            pend.splits = 0;
+        } else {
+            flush();
+        }
         if (launch) cfd::launch_gn(g, B, st);
         return Act{nbuf, in.C(), nullptr, 0, in.H, in.W};
     };
@@ -440,7 +465,12 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         a.Cout = cout;
         a.M = B * a.Hout * a.Wout;
         a.K = ks * ks * a.Ctot;
-        if (launch) cfd::launch_conv(a, plan_checked(a, kSplitCap), st);
+        flush();
+        const cfd::ConvPlan plan = plan_checked(a, kSplitCap);
+        if (launch && cfd::launch_conv(a, plan, st, /*defer=*/true) > 1) {
+            pend.a = a;
+            pend.splits = plan.splits;
+        }
     };
 
     std::vector<std::pair<Act, int>> stack;  // (tensor, skip index)
@@ -479,6 +509,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 // the current activation must live in its own skip buffer
                 float* dst = hsbuf[hs_i];
                 if (cur.a != dst) {
+                    flush();
                     if (launch)
                         CFD_HIP(hipMemcpyAsync(dst, cur.a, sizeof(float) * (size_t)B * cur.H * cur.W * cur.Ca,
                                                hipMemcpyDeviceToDevice, st));
@@ -506,11 +537,9 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 const size_t nout = (size_t)B * cur.H * cur.W * r.cout;
                 // h = in_layers(x) + emb_layers(emb)   (unet.py:236-254)
                 const Act xin = gn(cur, r.pre + ".in_layers.0", 1, &rec.ss1, &rec.st1);
-                float* hb = tape ? keep(nout) : tmp;
-                conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, hb);
-                rec.h1 = hb;
-                const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
-                // skip(x) + out_layers(h)   (unet.py:255-256)
+                // skip(x) first (its split-K reduction is flushed by the next
+                // convolution), so that in_layers' deferred reduction meets the
+                // out_layers GroupNorm directly   (unet.py:255-256)
                 const float* resp;
                 if (r.cin != r.cout) {
                     conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
@@ -519,6 +548,10 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     CFD_REQUIRE(cur.b == nullptr, CFD_ESTATE, "identity skip on a concatenated input");
                     resp = cur.a;
                 }
+                float* hb = tape ? keep(nout) : tmp;
+                conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, hb);
+                rec.h1 = hb;
+                const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
                 const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2);
                 float* out = dest(cur.a, cur.b, nout);
                 conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
@@ -537,6 +570,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 rec.qkv = qb;
                 rec.o = ob;
                 rec.lse = aa.lse;
+                flush();
                 if (launch) {
                     if (h->compute == CFD_COMPUTE_SPLIT_F16 && (at.ch == 32 || at.ch == 64 || at.ch == 128))
                         cfd::launch_attention_split(aa, at.ch, at.heads, B, kvws, st);
@@ -576,12 +610,14 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 a.Cout = c.out_channels;
                 a.M = B * cur.H * cur.W;
                 a.K = 9 * cur.Ca;
+                flush();
                 if (launch) cfd::launch_conv_out(a, st);
                 break;
             }
         }
         if (recs) (*recs)[si] = rec;
     }
+    flush();
 }
 
 

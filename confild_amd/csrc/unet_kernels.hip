@@ -249,10 +249,40 @@ __global__ __launch_bounds__(512) void gn_fused_reg_kernel(GnArgs a) {
     __shared__ double red[2][NT];
     __shared__ float sh[2][32];
     f4 v[IPT];
+    if (a.kpart && c < a.C1) {
+        // split-K source (GnArgs::kpart): reduce, epilogue, store x, keep it
+        const int64_t slab = (int64_t)a.B * HW * a.C1;
+        f4 kb = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        const int p = r0 + k * rows;
-        v[k] = act && p < HW ? *(const f4*)(src + (int64_t)p * ld) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j) {
+            if (a.kbias) kb[j] = a.kbias[c + j];
+            if (a.kemb) ke[j] = a.kemb[b * a.kemb_stride + c + j];
+        }
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int p = r0 + k * rows;
+            f4 x = {0.f, 0.f, 0.f, 0.f};
+            if (act && p < HW) {
+                const int64_t i = (b * HW + p) * a.C1 + c;
+                x = *(const f4*)(a.kpart + i);
+                for (int sp = 1; sp < a.ksplits; ++sp) x += *(const f4*)(a.kpart + sp * slab + i);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float y = a.kbias ? x[j] + kb[j] : x[j];
+                    if (a.kemb) y = y + ke[j];
+                    if (a.kres) y = a.kres[i + j] + y;
+                    x[j] = y;
+                }
+                *(f4*)(a.kx + i) = x;
+            }
+            v[k] = x;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int p = r0 + k * rows;
+            v[k] = act && p < HW ? *(const f4*)(src + (int64_t)p * ld) : f4{0.f, 0.f, 0.f, 0.f};
+        }
     }
     double s = 0, s2 = 0;
 #pragma unroll
@@ -1015,12 +1045,22 @@ static int env_int(const char* name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 
+bool gn_takes_splitk(const GnArgs& a, int B) {
+    (void)B;
+    static const int fused = env_int("CFD_GN_FUSED", 1);
+    static const int ksrc = env_int("CFD_GN_SPLITK", 1);
+    if (!ksrc || fused != 1 || a.Ctot % 128 != 0 || a.C1 % 4 != 0) return false;
+    const int rows = 512 / (a.Ctot / 128);
+    return ceil_div(a.HW, rows) <= 32;
+}
+
 void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     CFD_REQUIRE(a0.Ctot % 32 == 0 && a0.C1 % 4 == 0 && a0.C2 % 4 == 0 && a0.Ctot <= 1024, CFD_ESHAPE,
                 "GroupNorm32 needs channels % 32 == 0 (<= 1024)");
     GnArgs a = a0;
     a.nchunks = gn_chunks(a.HW);
     a.B = B;
+    CFD_REQUIRE(!a.kpart || gn_takes_splitk(a, B), CFD_ESTATE, "internal: split-K source on a GroupNorm path without it");
     static const int fused = env_int("CFD_GN_FUSED", 1);
     if (fused && a.Ctot % 128 == 0) {
         const int nq = a.Ctot / 128, rows = 512 / nq;
@@ -1096,7 +1136,13 @@ static void launch_conv_tiles(const ConvArgs& a, const ConvPlan& p, dim3 grid, h
         hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE, MODE>), grid, dim3(256), 0, st, a);
 }
 
-void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
+void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st) {
+    const int64_t total4 = (int64_t)a.M * a.Cout / 4;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0, st, a, splits);
+    check_launch("splitk_reduce_kernel");
+}
+
+int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer) {
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
     CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot, CFD_ESHAPE, "conv K mismatch");
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
@@ -1112,11 +1158,8 @@ void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
     else
         launch_conv_tiles<false, 0>(a, p, grid, st);
     check_launch("conv_gemm_kernel");
-    if (p.splits > 1) {
-        const int64_t total4 = (int64_t)a.M * a.Cout / 4;
-        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0, st, a, p.splits);
-        check_launch("splitk_reduce_kernel");
-    }
+    if (p.splits > 1 && !defer) launch_splitk_reduce(a, p.splits, st);
+    return p.splits;
 }
 
 void launch_conv_in(const ConvArgs& a, hipStream_t st) {

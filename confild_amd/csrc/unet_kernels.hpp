@@ -18,6 +18,17 @@ struct GnArgs {
     int silu;
     int nchunks;
     int B;
+    // Optional: src1 is the still-unreduced output of a split-K convolution
+    // (launch_conv with defer).  This kernel then forms x = sum_s kpart[s]
+    // (+ kbias) (+ kemb[b]), then kres + x -- splitk_reduce's order, so x is
+    // bit-identical -- writes it to kx (= the convolution's output) and
+    // normalises it: one launch and one pass over x fewer.
+    const float* kpart;  // (ksplits, B*HW, C1) partial slab, or null
+    const float* kbias;
+    const float* kemb;
+    const float* kres;
+    float* kx;
+    int ksplits, kemb_stride;
 };
 
 struct ConvArgs {
@@ -88,10 +99,16 @@ struct ConvPlan {
 int gn_chunks(int HW);
 // GroupNorm statistics + normalise (+SiLU) into a.out
 void launch_gn(const GnArgs& a, int B, hipStream_t st);
+// whether launch_gn runs the register-resident kernel for this shape (the only
+// one that accepts a split-K source, GnArgs::kpart)
+bool gn_takes_splitk(const GnArgs& a, int B);
 // part_cap_floats: split-K slab available per 8 samples (plans depend on the
 // per-sample shape only, never on the batch)
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats);
-void launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st);
+// Returns the split count.  With defer and splits > 1 the reduction is not
+// launched: the caller runs launch_splitk_reduce or hands the slab to launch_gn.
+int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer = false);
+void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st);
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
 void launch_conv_out(const ConvArgs& a, hipStream_t st);
 void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t st);

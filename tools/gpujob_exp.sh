@@ -2,8 +2,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
-for r in 1 2; do
-timeout -k 10 200 python tools/kbench.py unet --unet-compute split_f16 > gpurun_out/kb_u.log 2>&1 || { cat gpurun_out/kb_u.log; exit 2; }
-grep kernel gpurun_out/kb_u.log
-done
-bash tools/gpujob_prof_unet.sh | head -8
+bash tools/gpujob_ab.sh
