@@ -113,6 +113,20 @@ __device__ __forceinline__ float sin1_cw(float x) {
     return __uint_as_float(__float_as_uint(y) + (__float_as_uint(t) << 31));
 }
 
+// sin(x) with the hardware sine: x = r + q 2pi (q = rint(x / 2pi), Cody-Waite
+// with 2x sin1_cw's pi terms, exact for the same range), then v_sin_f32 on
+// r / 2pi revolutions (|r / 2pi| <= 1/2).  7 VALU + one transcendental (2 issue
+// slots) against sin1_cw's 13.
+__device__ __forceinline__ float sin_hw(float x) {
+    const float t = fmaf(x, 0.159154943091895335768f, 12582912.0f);
+    const float q = t - 12582912.0f;
+    float r = fmaf(q, -6.28125f, x);
+    r = fmaf(q, -0.001934051513671875f, r);
+    r = fmaf(q, -1.2554228305816650391e-06f, r);
+    r = fmaf(q, -2.4308402513106841524e-10f, r);
+    return __builtin_amdgcn_sinf(r * 0.159154943091895335768f);
+}
+
 template <bool PK>
 __device__ __forceinline__ f2 sin2_sel(f2 x) {
     if constexpr (PK) return sin2_cw(x);
@@ -418,7 +432,7 @@ __device__ __forceinline__ void split_chunk(const float (&x)[16], int e, Frag& h
 
 // EXP (timing experiments only, wrong results): bit 0 no weight streaming / barrier,
 // bit 1 no sine (x = scaled accumulator), bit 2 A-fragment prefetch two steps ahead
-template <int NB2, int EXP = 0>
+template <int NB2, int EXP = 0, bool HWSIN = false>
 __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
     constexpr int NK = 2 * NB2;    // 16-deep K chunks per layer
     constexpr int H = 32 * NB2;
@@ -493,7 +507,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
 #pragma unroll
                 for (int k = 1; k < 4; ++k)
                     if (k < p.d) a = fmaf(cn[k], w[k], a);
-                x[4 * qq + r] = sin1_cw(p.w0f * (a + fv[r]));
+                x[4 * qq + r] = HWSIN ? sin_hw(p.w0f * (a + fv[r])) : sin1_cw(p.w0f * (a + fv[r]));
             }
         }
         split_chunk(x, 0, NH[2 * J], NL[2 * J]);
@@ -575,7 +589,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
                 if constexpr (k < NKS) {
 #pragma unroll
                     for (int v = 16 * k / NKS; v < 16 * (k + 1) / NKS; ++v) {
-                        x[v] = (EXP & 2) ? prev[v] * me : sin1_cw(prev[v] * me);
+                        x[v] = (EXP & 2) ? prev[v] * me : HWSIN ? sin_hw(prev[v] * me) : sin1_cw(prev[v] * me);
                         asm volatile("" : "+v"(x[v]));  // keep it in this step (no sinking to the split)
                     }
                 }
@@ -613,7 +627,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
     }
     // the last layer's last block
 #pragma unroll
-    for (int v = 0; v < 16; ++v) x[v] = sin1_cw(prev[v] * mprev);
+    for (int v = 0; v < 16; ++v) x[v] = HWSIN ? sin_hw(prev[v] * mprev) : sin1_cw(prev[v] * mprev);
     {
         const int f0 = 32 * (NB2 - 1) + 4 * h;
 #pragma unroll
@@ -699,11 +713,11 @@ void launch_nb(SirenArgs a, int b, hipStream_t st) {
 }
 }  // namespace
 
-template <int NB2, int EXP = 0>
+template <int NB2, int EXP = 0, bool HWSIN = false>
 void launch_split32(SirenArgs a, int b, hipStream_t st) {
     constexpr int H = NB2 * 32;
     const size_t lds = sizeof(float) * ((size_t)2 * 2 * NB2 * 512 + (size_t)(a.nh + 1) * H + 8 * H);
-    const void* fn = (const void*)siren_split32<NB2, EXP>;
+    const void* fn = (const void*)siren_split32<NB2, EXP, HWSIN>;
     CFD_REQUIRE((int64_t)a.nh * H * H * 4 < 0x7fffffffLL, CFD_EARG, "weight image beyond the 2 GiB buffer range");
     CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the split-f16 decoder's LDS staging");
     CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -712,7 +726,7 @@ void launch_split32(SirenArgs a, int b, hipStream_t st) {
     for (int64_t b0 = 0; b0 < b; b0 += 65535) {
         a.b0 = b0;
         const int nb = (int)std::min<int64_t>(65535, b - b0);
-        hipLaunchKernelGGL((siren_split32<NB2, EXP>), dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
+        hipLaunchKernelGGL((siren_split32<NB2, EXP, HWSIN>), dim3((unsigned)tiles, nb), dim3(256), lds, st, a);
         check_launch("siren_split32");
     }
 }
@@ -724,6 +738,16 @@ bool siren_split32_supported(int H, int nh) {
 }
 
 void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
+    static const int hw = env_int("CFD_SIREN_HWSIN", 1, 0, 1);
+    if (hw) {
+        switch (H) {
+            case 64: return launch_split32<2, 0, true>(a, b, st);
+            case 128: return launch_split32<4, 0, true>(a, b, st);
+            case 256: return launch_split32<8, 0, true>(a, b, st);
+            case 384: return launch_split32<12, 0, true>(a, b, st);
+            default: break;
+        }
+    }
     switch (H) {
         case 64: return launch_split32<2>(a, b, st);
         case 128: return launch_split32<4>(a, b, st);
@@ -761,4 +785,18 @@ void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st) {
     }
 }
 
+__global__ void sine_probe_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int which) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = which == 1 ? sin_hw(x[i]) : sin1_cw(x[i]);
+}
+
 }  // namespace cfd
+
+extern "C" int cfd_sine_probe(const float* x, float* y, int64_t n, int which, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(x && y && n > 0 && (which == 0 || which == 1), CFD_EARG, "bad argument");
+        hipLaunchKernelGGL(cfd::sine_probe_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0,
+                           (hipStream_t)stream, x, y, n, which);
+        cfd::check_launch("sine_probe_kernel");
+    });
+}

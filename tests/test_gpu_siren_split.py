@@ -100,3 +100,28 @@ def test_split_f16_large_weights_scale(hip):
     f32, _ = _decode(net, "f32", coords, lat, ymax, ymin)
     e_s, e_f = (split - ref64).abs().max().item(), (f32 - ref64).abs().max().item()
     assert e_s <= 2 * e_f + 1e-7 * ref64.abs().max().item()
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_device_sine_is_fp32_accurate(hip, which):
+    """The decoder's sines (cfd_sine_probe: 0 = Cody-Waite pi + polynomial, 1 =
+    Cody-Waite 2 pi + v_sin_f32, the split32 default) against float64 sin over the
+    pre-activation range SIREN weights produce and well beyond (|x| <= 3000)
+    and near 0, absolute error (the activations enter the next layer as 22-bit
+    splits of values of order 1, so absolute error is what propagates).  Bounds:
+    the polynomial 2 ulp of 1 (2.4e-7; measured 1.2e-7); the hardware sine 5 ulp
+    (6e-7; measured 4.6e-7, v_sin_f32's own error).  The end-to-end decode error
+    against fp64 is the same with either (test_split_f16_has_fp32_accuracy runs
+    the default, v_sin_f32)."""
+    from confild_amd import _lib
+    g = torch.Generator().manual_seed(5)
+    x = torch.cat([torch.rand(1 << 20, generator=g) * 200 - 100, torch.rand(1 << 18, generator=g) * 6000 - 3000,
+                   torch.rand(1 << 16, generator=g) * 2e-3 - 1e-3, torch.tensor([0.0, 3.14159265, -3.14159265])])
+    xd = x.to(DEV)
+    y = torch.empty_like(xd)
+    _lib.check(_lib.load().cfd_sine_probe(_lib.ptr(xd), _lib.ptr(y), x.numel(), which, _lib.stream_of(DEV)),
+               "cfd_sine_probe")
+    ref = torch.sin(x.double())
+    err = (y.cpu().double() - ref).abs()
+    print(f"sine {which}: max abs err {err.max().item():.3e}")
+    assert err.max().item() <= (2.4e-7 if which == 0 else 6e-7)
