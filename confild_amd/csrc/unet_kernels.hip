@@ -249,7 +249,9 @@ __global__ __launch_bounds__(512) void gn_fused_reg_kernel(GnArgs a) {
     __shared__ double red[2][NT];
     __shared__ float sh[2][32];
     f4 v[IPT];
-    if (a.kpart && c < a.C1) {
+    bool ksrc = false;
+    if constexpr (IPT <= 16) ksrc = a.kpart && c < a.C1;  // (gn_takes_splitk: IPT <= 16)
+    if (ksrc) {  // constant false for IPT > 16: the branch folds away
         // split-K source (GnArgs::kpart): reduce, epilogue, store x, keep it
         const int64_t slab = (int64_t)a.B * HW * a.C1;
         f4 kb = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
@@ -258,24 +260,44 @@ __global__ __launch_bounds__(512) void gn_fused_reg_kernel(GnArgs a) {
             if (a.kbias) kb[j] = a.kbias[c + j];
             if (a.kemb) ke[j] = a.kemb[b * a.kemb_stride + c + j];
         }
+        // every load first (the partials, then the residual), every store after:
+        // kx may alias neither input, but the compiler cannot know that, and an
+        // interleaved store would serialise the loads behind it
+        const float* __restrict__ kpart = a.kpart;
+        const float* __restrict__ kres = a.kres;
+        float* __restrict__ kx = a.kx;
+        const int64_t ib = (b * HW + r0) * a.C1 + c, istep = (int64_t)rows * a.C1;
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const int p = r0 + k * rows;
-            f4 x = {0.f, 0.f, 0.f, 0.f};
+            v[k] = act && p < HW ? *(const f4*)(kpart + ib + k * istep) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+        for (int sp = 1; sp < a.ksplits; ++sp) {
+#pragma unroll
+            for (int k = 0; k < IPT; ++k) {
+                const int p = r0 + k * rows;
+                if (act && p < HW) v[k] += *(const f4*)(kpart + sp * slab + ib + k * istep);
+            }
+        }
+        f4 rs[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int p = r0 + k * rows;
+            rs[k] = kres && act && p < HW ? *(const f4*)(kres + ib + k * istep) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int p = r0 + k * rows;
             if (act && p < HW) {
-                const int64_t i = (b * HW + p) * a.C1 + c;
-                x = *(const f4*)(a.kpart + i);
-                for (int sp = 1; sp < a.ksplits; ++sp) x += *(const f4*)(a.kpart + sp * slab + i);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    float y = a.kbias ? x[j] + kb[j] : x[j];
+                    float y = a.kbias ? v[k][j] + kb[j] : v[k][j];
                     if (a.kemb) y = y + ke[j];
-                    if (a.kres) y = a.kres[i + j] + y;
-                    x[j] = y;
+                    if (kres) y = rs[k][j] + y;
+                    v[k][j] = y;
                 }
-                *(f4*)(a.kx + i) = x;
+                *(f4*)(kx + ib + k * istep) = v[k];
             }
-            v[k] = x;
         }
     } else {
 #pragma unroll
@@ -1051,7 +1073,7 @@ bool gn_takes_splitk(const GnArgs& a, int B) {
     static const int ksrc = env_int("CFD_GN_SPLITK", 1);
     if (!ksrc || fused != 1 || a.Ctot % 128 != 0 || a.C1 % 4 != 0) return false;
     const int rows = 512 / (a.Ctot / 128);
-    return ceil_div(a.HW, rows) <= 32;
+    return ceil_div(a.HW, rows) <= 16;
 }
 
 void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
