@@ -748,6 +748,80 @@ __global__ void conv_out_kernel(ConvArgs a) {
     }
 }
 
+// Forward last convolution, vectorised: LP = Ctot/4 lanes per output pixel
+// (64/LP pixels per wave), each lane a float4 of channels per tap; per-tap
+// bounds, no division in the loop; weights (Cout, 9, Ctot) staged in LDS.
+// Fixed summation order (lane partial over taps, then a butterfly), so every
+// sample's output is independent of the batch.
+__global__ __launch_bounds__(256) void conv_out_vec_kernel(ConvArgs a, int LP) {
+    extern __shared__ __attribute__((aligned(16))) float wsm[];
+    for (int i = threadIdx.x; i < a.Cout * a.K; i += blockDim.x) wsm[i] = a.w[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int ppw = 64 / LP;
+    const int64_t m = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * ppw + lane / LP;
+    const int c = 4 * (lane % LP);
+    const int HW = a.Hout * a.Wout;
+    const int64_t mm = m < a.M ? m : a.M - 1;
+    const int b = (int)(mm / HW), rem = (int)(mm - (int64_t)b * HW), oy = rem / a.Wout, ox = rem - oy * a.Wout;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int tap = 0; tap < 9; ++tap) {
+        const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+        if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
+        const f4 v = *(const f4*)(a.src1 + (((int64_t)b * a.Hin + iy) * a.Win + ix) * a.C1 + c);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            if (n < a.Cout) {
+                const f4 w = *(const f4*)(wsm + (n * 9 + tap) * a.Ctot + c);
+                s[n] = fmaf(w[0], v[0], fmaf(w[1], v[1], fmaf(w[2], v[2], fmaf(w[3], v[3], s[n]))));
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        if (n >= a.Cout) break;
+        float v = s[n];
+        for (int o = LP >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane % LP == 0 && m < a.M) a.out[m * a.Cout + n] = a.bias ? v + a.bias[n] : v;
+    }
+}
+
+// Forward first convolution, C1 <= 4 -> Cout: one thread per (pixel, 4 output
+// channels), weights staged in LDS as (tap, c, Cout) so a thread reads a float4.
+__global__ __launch_bounds__(256) void conv_in_vec_kernel(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float wsm[];  // (9, C1, Cout)
+    const int C1 = a.C1, Cout = a.Cout;
+    for (int i = threadIdx.x; i < 9 * C1 * Cout; i += blockDim.x) {
+        const int n = i % Cout, tc = i / Cout, tap = tc / C1, cc = tc % C1;
+        wsm[i] = a.w[((int64_t)n * 9 + tap) * C1 + cc];
+    }
+    __syncthreads();
+    const int nq = Cout / 4;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)a.M * nq) return;
+    const int n0 = 4 * (int)(idx % nq);
+    const int64_t m = idx / nq;
+    const int HW = a.Hout * a.Wout;
+    const int b = (int)(m / HW), rem = (int)(m - (int64_t)b * HW), oy = rem / a.Wout, ox = rem - oy * a.Wout;
+    f4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int tap = 0; tap < 9; ++tap) {
+        const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+        if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
+        const float* px = a.src1 + (((int64_t)b * a.Hin + iy) * a.Win + ix) * C1;
+        for (int cc = 0; cc < C1; ++cc) {
+            const float v = px[cc];
+            const f4 w = *(const f4*)(wsm + (tap * C1 + cc) * Cout + n0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[j] = fmaf(w[j], v, s[j]);
+        }
+    }
+    if (a.bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] += a.bias[n0 + j];
+    }
+    *(f4*)(a.out + m * Cout + n0) = s;
+}
+
 // ---------------------------------------------------------------------------
 // K4: QKVAttentionLegacy.  qkv (B, T, 3C) with head h's q/k/v at channels
 // h*3*CH + {0, CH, 2CH} + i (the legacy "split heads before qkv" order,
@@ -1185,6 +1259,13 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer
 }
 
 void launch_conv_in(const ConvArgs& a, hipStream_t st) {
+    if (!a.tmode && a.Cout % 4 == 0 && a.C1 <= 4 && (size_t)9 * a.C1 * a.Cout * 4 <= 64 * 1024) {
+        const int64_t n = (int64_t)a.M * (a.Cout / 4);
+        hipLaunchKernelGGL(conv_in_vec_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256),
+                           sizeof(float) * 9 * a.C1 * a.Cout, st, a);
+        check_launch("conv_in_vec_kernel");
+        return;
+    }
     const int64_t n = (int64_t)a.M * a.Cout;
     hipLaunchKernelGGL(conv_in_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, a);
     check_launch("conv_in_kernel");
@@ -1192,6 +1273,15 @@ void launch_conv_in(const ConvArgs& a, hipStream_t st) {
 
 void launch_conv_out(const ConvArgs& a, hipStream_t st) {
     CFD_REQUIRE(a.Cout <= 4, CFD_ESHAPE, "out_channels must be <= 4");
+    const int LP = a.Ctot / 4;
+    if (!a.tmode && a.Ctot % 4 == 0 && a.C1 == a.Ctot && LP >= 1 && LP <= 64 && (LP & (LP - 1)) == 0 &&
+        (size_t)a.Cout * a.K * 4 <= 64 * 1024) {
+        const int64_t waves = ceil_div(a.M, 64 / LP);
+        hipLaunchKernelGGL(conv_out_vec_kernel, dim3((unsigned)ceil_div(waves, 4)), dim3(256),
+                           sizeof(float) * a.Cout * a.K, st, a, LP);
+        check_launch("conv_out_vec_kernel");
+        return;
+    }
     hipLaunchKernelGGL(conv_out_kernel, dim3((unsigned)ceil_div(a.M, 4)), dim3(256), 0, st, a);
     check_launch("conv_out_kernel");
 }
