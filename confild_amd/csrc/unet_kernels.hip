@@ -1192,7 +1192,7 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // (or rank shard) it is computed in.  Knobs (development): CFD_CONV_BM
     // (0 = auto), CFD_CONV_TARGET_WG.
     static const int force_bm = env_int("CFD_CONV_BM", 0);
-    static const int target = env_int("CFD_CONV_TARGET_WG", 1024);
+    static const int target = env_int("CFD_CONV_TARGET_WG", 768);
     ConvPlan p;
     const int64_t mn = (int64_t)8 * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;
