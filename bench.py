@@ -70,6 +70,20 @@ def measured_traffic(mode, latents, npts):
     return rec["traffic_bytes_per_launch"] * (latents * npts) / ref_pairs
 
 
+def measured_mfma_util(kname):
+    """Matrix-pipe busy fraction and held clock of the decoder kernel from the
+    committed rocprofv3 record (tools/gpujob_mfma_util.sh, tools/mfma_util.py)."""
+    try:
+        rec = json.load(open(os.path.join(ROOT, "profiles", "r01_mfma_util.json")))
+    except (OSError, ValueError):
+        return None
+    for k, v in rec.items():
+        if k.startswith(f"cfd::{kname}<") and isinstance(v, dict):
+            return {"mfma_busy_frac": v["mfma_busy_frac"], "held_clock_ghz": v["held_clock_ghz"],
+                    "source": "profiles/r01_mfma_util.json"}
+    return None
+
+
 def siren_flops_per_pair(d, L, c, nh, H):
     return 2 * (d * H + nh * H * H + H * c)
 
@@ -253,7 +267,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)", "achieved": achieved,
                          "peak": peak, "peak_basis": peak_basis, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": measured_traffic(mode, B * S, GRID ** 3), "flops_per_launch": flops,
-                         "launch_ms": dec_s * 1e3,
+                         "launch_ms": dec_s * 1e3, "pmc": measured_mfma_util(kname),
                          "unet_share_ms": (elapsed / args.steps - dec_s) * 1e3},
             "cpu_baseline": cpu,
         }
