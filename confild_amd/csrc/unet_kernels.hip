@@ -423,7 +423,21 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    // XCD-contiguous tile order (a.xcd): workgroup L runs on XCD L % 8 (round-robin
+    // dispatch); hand XCD x the x-th contiguous run of the (m, n, split) tiles,
+    // splits fastest, so the workgroups sharing an XCD's L2 share activation rows
+    // (the 3x3 halo and every split of one pixel tile) instead of striding the image.
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (a.xcd) {
+        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
+        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
+        bz = Lp % gz;
+        by = (Lp / gz) % gy;
+        bx = Lp / (gz * gy);
+    }
+    const int m0 = bx * BM, n0 = by * BN;
     const int HWo = a.Hout * a.Wout;
     const int kq = tid & 7, rsub = tid >> 3;  // 8 threads per 32-float row
 
@@ -465,7 +479,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     }
     const int nkt = a.K / BK;
     const int per = (nkt + gridDim.z - 1) / gridDim.z;
-    const int kt0 = blockIdx.z * per;
+    const int kt0 = bz * per;
     const int kt1 = min(nkt, kt0 + per);
     // wave-uniform K position: (dy, dx) tap and channel base, advanced per tile
     int cb = 0, dy = 0, dx = 0;
@@ -645,7 +659,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             for (int j = 0; j < TN; ++j) acc[i][j] *= a.acc_scale;
     }
     if (gridDim.z > 1) {
-        float* part = a.part + (int64_t)blockIdx.z * a.M * a.Cout;
+        float* part = a.part + (int64_t)bz * a.M * a.Cout;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1245,14 +1259,18 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer
     CFD_REQUIRE(!a.tmode || ((a.stride == 1 || a.stride == 2) && !a.up), CFD_ESHAPE, "transposed conv: stride 1|2");
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
     CFD_REQUIRE(!(a.tmode && a.wbf), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
+    static const int xcd = env_int("CFD_CONV_XCD", 1);
+    ConvArgs b = a;
+    b.xcd = xcd ? 1 : 0;
+    const ConvArgs& a_ = b;
     if (a.tmode)
-        launch_conv_tiles<true, 0>(a, p, grid, st);
+        launch_conv_tiles<true, 0>(a_, p, grid, st);
     else if (a.wbf && a.wlo)
-        launch_conv_tiles<false, 2>(a, p, grid, st);
+        launch_conv_tiles<false, 2>(a_, p, grid, st);
     else if (a.wbf)
-        launch_conv_tiles<false, 1>(a, p, grid, st);
+        launch_conv_tiles<false, 1>(a_, p, grid, st);
     else
-        launch_conv_tiles<false, 0>(a, p, grid, st);
+        launch_conv_tiles<false, 0>(a_, p, grid, st);
     check_launch("conv_gemm_kernel");
     if (p.splits > 1 && !defer) launch_splitk_reduce(a, p.splits, st);
     return p.splits;

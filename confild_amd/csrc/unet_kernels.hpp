@@ -50,6 +50,7 @@ struct ConvArgs {
     int Cout;
     int emb_stride;
     int M, K;
+    int xcd;             // XCD-contiguous workgroup order (set by launch_conv; CFD_CONV_XCD=0: off)
 };
 
 struct AttnArgs {
