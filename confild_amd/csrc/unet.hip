@@ -27,6 +27,7 @@ struct UParam {
     int tpack = 0;       // input-gradient pack: 0 none, 1 transposed (Cin, taps, Cout), 2 upsample 4x4 (Cin, 16, Cout)
     size_t toffset = 0;  // floats into the transposed arena
     float split_inv = 1.f;  // split compute: 1 / s, s = power-of-two scale of this conv weight
+    float tsplit_inv = 1.f; // the same for the input-gradient pack
 };
 
 struct ResSpec {
@@ -68,6 +69,8 @@ struct cfd_unet {
     uint16_t* arena_bf = nullptr;  // bf16 copy of the conv weights, same offsets as arena
     uint16_t* arena_hi = nullptr;  // split compute: f16 hi / lo parts of the scaled conv weights
     uint16_t* arena_lo = nullptr;
+    uint16_t* arena_thi = nullptr;  // split compute: f16 hi / lo parts of the scaled input-gradient packs
+    uint16_t* arena_tlo = nullptr;
     int compute = CFD_COMPUTE_SPLIT_F16;
 };
 
@@ -239,6 +242,19 @@ uint16_t to_bf16(float f) {
     std::memcpy(&u, &f, 4);
     if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
     return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+// split compute: f16 hi / lo parts and 1/s of an input-gradient pack into a
+// (nothing in the other modes: their transposed convolutions run in fp32)
+void PTS(const cfd_unet* h, const std::string& key, cfd::ConvArgs* a) {
+    static const bool on = !getenv("CFD_VJP_SPLIT") || atoi(getenv("CFD_VJP_SPLIT")) != 0;  // 0: fp32 (A/B)
+    if (h->compute != CFD_COMPUTE_SPLIT_F16 || !on) return;
+    auto it = h->index.find(key);
+    CFD_REQUIRE(it != h->index.end() && h->params[it->second].tpack, CFD_EKEY, "internal: missing conv " + key);
+    const auto& p = h->params[it->second];
+    a->wbf = h->arena_thi + p.toffset;
+    a->wlo = h->arena_tlo + p.toffset;
+    a->acc_scale = p.tsplit_inv;
 }
 
 const float* PT(const cfd_unet* h, const std::string& key) {
@@ -657,6 +673,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         a.C1 = cin;
         a.Ctot = cin;
         a.w = PT(h, key);
+        PTS(h, key, &a);
         a.out = out;
         a.part = splitk;
         a.Hin = Hin;
@@ -826,6 +843,8 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             CFD_HIP(hipMalloc(&h->arena_bf, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
             CFD_HIP(hipMalloc(&h->arena_hi, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
             CFD_HIP(hipMalloc(&h->arena_lo, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
+            CFD_HIP(hipMalloc(&h->arena_thi, sizeof(uint16_t) * std::max<size_t>(h->arena_t_floats, 4)));
+            CFD_HIP(hipMalloc(&h->arena_tlo, sizeof(uint16_t) * std::max<size_t>(h->arena_t_floats, 4)));
             if (const char* e = getenv("CFD_UNET_COMPUTE")) h->compute = atoi(e);
             const int half = cfg->model_channels / 2;
             // freqs = exp(-ln(10000) * arange(half, fp32) / half) in fp32 (nn.py:129-131)
@@ -852,6 +871,8 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->arena_bf);
     (void)hipFree(h->arena_hi);
     (void)hipFree(h->arena_lo);
+    (void)hipFree(h->arena_thi);
+    (void)hipFree(h->arena_tlo);
     delete h;
 }
 
@@ -952,6 +973,21 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
                             }
             }
             CFD_HIP(hipMemcpy(h->arena_t + p.toffset, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
+            // split compute: the same power-of-two scaled hi / lo split as the forward pack
+            float amax = 0.f;
+            for (float v : pk) amax = std::max(amax, std::fabs(v));
+            int ex = 0;
+            if (amax > 0.f) std::frexp(amax, &ex);
+            const float sc = std::ldexp(1.0f, -ex);
+            p.tsplit_inv = std::ldexp(1.0f, ex);
+            std::vector<_Float16> thi(pk.size()), tlo(pk.size());
+            for (size_t e = 0; e < pk.size(); ++e) {
+                const float v = pk[e] * sc;
+                thi[e] = (_Float16)v;
+                tlo[e] = (_Float16)(v - (float)thi[e]);
+            }
+            CFD_HIP(hipMemcpy(h->arena_thi + p.toffset, thi.data(), pk.size() * 2, hipMemcpyHostToDevice));
+            CFD_HIP(hipMemcpy(h->arena_tlo + p.toffset, tlo.data(), pk.size() * 2, hipMemcpyHostToDevice));
         }
         p.set = true;
     });

@@ -1258,12 +1258,14 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
     CFD_REQUIRE(!a.tmode || ((a.stride == 1 || a.stride == 2) && !a.up), CFD_ESHAPE, "transposed conv: stride 1|2");
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
-    CFD_REQUIRE(!(a.tmode && a.wbf), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
+    CFD_REQUIRE(!(a.tmode && a.wbf && !a.wlo), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
     static const int xcd = env_int("CFD_CONV_XCD", 1);
     ConvArgs b = a;
     b.xcd = xcd ? 1 : 0;
     const ConvArgs& a_ = b;
-    if (a.tmode)
+    if (a.tmode && a.wlo)
+        launch_conv_tiles<true, 2>(a_, p, grid, st);
+    else if (a.tmode)
         launch_conv_tiles<true, 0>(a_, p, grid, st);
     else if (a.wbf && a.wlo)
         launch_conv_tiles<false, 2>(a_, p, grid, st);

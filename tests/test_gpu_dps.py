@@ -177,3 +177,25 @@ def test_dps_batch_equals_single_chains(hip):
         assert torch.equal(one, full[s:s + 1]), s
         assert torch.equal(sampler.distances[:, 0], dfull[:, s]), s
     assert torch.isfinite(full).all()
+
+
+@pytest.mark.parametrize("name", ["tiny16", "cfgB64"])
+def test_unet_input_vjp_split_is_fp32_level(hip, name):
+    """Split-f16 transposed convolutions (default compute): the input-gradient's
+    error against float64 autograd stays within 2x the fp32 kernels' error
+    (+1e-7 of the gradient scale), as for the forward (test_gpu_unet_split.py)."""
+    g, cfg, sd, m = _unet(name)
+    x = torch.from_numpy(g["x"])
+    t = torch.from_numpy(g["t"])
+    d_eps = torch.from_numpy(synth.normal(5, f"{name}/deps", tuple(x.shape)))
+    xr = x.double().requires_grad_()
+    eps_ref = ou.forward({k: v.double() for k, v in sd.items()}, cfg, xr, t)
+    (gx64,) = torch.autograd.grad(eps_ref, xr, d_eps.double())
+    err = {}
+    for mode in ("fp32", "split_f16"):
+        m.set_compute(mode)
+        m.forward_tape(x.to(DEV), t.to(DEV))
+        err[mode] = float((m.input_vjp(d_eps.to(DEV)).cpu().double() - gx64).abs().max())
+    m.set_compute("split_f16")
+    scale = float(gx64.abs().max())
+    assert err["split_f16"] <= 2 * err["fp32"] + 1e-7 * scale, (err, scale)
