@@ -138,8 +138,9 @@ int  cfd_sched_step(const cfd_sched* s, int kind, int clip, const float* x, cons
 int  cfd_randn(float* out, int64_t n, uint64_t seed, uint64_t counter, uint64_t offset, void* stream);
 /* Diagnostic: y = sin(x) by the decoder's device sine -- which 0: Cody-Waite pi
  * reduction + degree-9 polynomial (sin_cw family), 1: Cody-Waite 2pi reduction +
- * v_sin_f32 (the split32 decoder's default).  Used by the tests to bound both
- * against float64 (components.py:19-25 Sine = torch.sin). */
+ * v_sin_f32, 2: reduction in revolutions (two-float 1/2pi) + v_sin_f32 (the
+ * split32 decoder's default).  Used by the tests to bound each against float64
+ * (components.py:19-25 Sine = torch.sin). */
 int  cfd_sine_probe(const float* x, float* y, int64_t n, int which, void* stream);
 /* Latent de-normalisation (scripts/inference.py:59-61): y = (x+1)*(max-min)/2 + min,
  * max/min broadcast over the trailing `period` elements (period=1: scalars). */
