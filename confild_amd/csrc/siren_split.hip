@@ -755,9 +755,9 @@ void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
     static const int hw = env_int("CFD_SIREN_HWSIN", 2, 0, 2);
     if (hw) {
         switch (H) {
-            case 64: return launch_split32<2, 0, 1>(a, b, st);
-            case 128: return launch_split32<4, 0, 1>(a, b, st);
-            case 256: return launch_split32<8, 0, 1>(a, b, st);
+            case 64: return hw == 2 ? launch_split32<2, 0, 2>(a, b, st) : launch_split32<2, 0, 1>(a, b, st);
+            case 128: return hw == 2 ? launch_split32<4, 0, 2>(a, b, st) : launch_split32<4, 0, 1>(a, b, st);
+            case 256: return hw == 2 ? launch_split32<8, 0, 2>(a, b, st) : launch_split32<8, 0, 1>(a, b, st);
             case 384: return hw == 2 ? launch_split32<12, 0, 2>(a, b, st) : launch_split32<12, 0, 1>(a, b, st);
             default: break;
         }
