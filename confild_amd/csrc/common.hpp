@@ -58,6 +58,23 @@ inline void check_launch(const char* what) {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Makes `device` current for the scope and restores the caller's device on
+// exit, so an entry point never changes the calling process's (or torch's)
+// current HIP device.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int device) {
+        CFD_HIP(hipGetDevice(&prev));
+        if (prev != device) CFD_HIP(hipSetDevice(device));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 // fp32 sine, branch-free.  |x| < 39000: Cody-Waite reduction by pi with a
 // 4-term split of pi (exact reduction in that range, the SLEEF single-precision
 // scheme), then a degree-9 odd minimax polynomial on [-pi/2, pi/2] (~3.5 ulp).

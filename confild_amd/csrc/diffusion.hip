@@ -203,7 +203,7 @@ struct cfd_sched {
 extern "C" int cfd_sched_create(const float* host_coefs, int n_t, int device, cfd_sched** out) {
     return cfd::guard([&] {
         CFD_REQUIRE(host_coefs && out && n_t > 0, CFD_EARG, "bad argument");
-        CFD_HIP(hipSetDevice(device));
+        cfd::DeviceGuard dg(device);
         auto* s = new cfd_sched();
         s->n_t = n_t;
         s->device = device;

@@ -603,7 +603,7 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_REQUIRE(NB == 1 || NB == 2 || NB == 3 || NB == 4 || NB == 6 || NB == 8 || NB == 12 || NB == 16 ||
                         NB == 24 || NB == 32,
                     CFD_EARG, "hidden_features must be 16*{1,2,3,4,6,8,12,16,24,32}");
-        CFD_HIP(hipSetDevice(device));
+        cfd::DeviceGuard dg(device);
         auto* h = new cfd_siren();
         h->cfg = *cfg;
         if (h->cfg.w0 == 0.f) h->cfg.w0 = 30.f;
@@ -666,7 +666,7 @@ extern "C" int cfd_siren_param_info(const cfd_siren* h, int idx, const char** ke
 extern "C" int cfd_siren_set_param(cfd_siren* h, const char* key, const float* host, size_t n) {
     return cfd::guard([&] {
         CFD_REQUIRE(h && key && host, CFD_EARG, "null argument");
-        CFD_HIP(hipSetDevice(h->device));
+        cfd::DeviceGuard dg(h->device);
         const std::string k(key);
         cfd::SirenParam* prm = nullptr;
         for (auto& p : h->params)

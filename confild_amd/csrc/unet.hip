@@ -830,7 +830,7 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
         const int levels_down = cfg->n_mult - 1;
         CFD_REQUIRE(cfg->image_size > 0 && (cfg->image_size >> levels_down) << levels_down == cfg->image_size,
                     CFD_EARG, "image_size must be divisible by 2^(len(channel_mult)-1)");
-        CFD_HIP(hipSetDevice(device));
+        cfd::DeviceGuard dg(device);
         auto* h = new cfd_unet();
         h->cfg = *cfg;
         h->device = device;
@@ -901,7 +901,7 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
         CFD_REQUIRE(it != h->index.end(), CFD_EKEY, std::string("unknown U-Net parameter key: ") + key);
         auto& p = h->params[it->second];
         CFD_REQUIRE(n == p.count, CFD_ESHAPE, std::string("size mismatch for ") + key);
-        CFD_HIP(hipSetDevice(h->device));
+        cfd::DeviceGuard dg(h->device);
         switch (p.pack) {
             case Pack::Raw:
                 CFD_HIP(hipMemcpy(h->arena + p.offset, host, n * 4, hipMemcpyHostToDevice));
@@ -1005,7 +1005,7 @@ extern "C" int cfd_unet_set_compute(cfd_unet* h, int compute) {
 extern "C" int cfd_unet_set_time_freqs(cfd_unet* h, const float* host, int n) {
     return cfd::guard([&] {
         CFD_REQUIRE(h && host && n == h->cfg.model_channels / 2, CFD_EARG, "freqs must have model_channels/2 entries");
-        CFD_HIP(hipSetDevice(h->device));
+        cfd::DeviceGuard dg(h->device);
         CFD_HIP(hipMemcpy(h->freqs, host, sizeof(float) * n, hipMemcpyHostToDevice));
     });
 }

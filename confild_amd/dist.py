@@ -77,7 +77,7 @@ def broadcast_module(module: torch.nn.Module, src: int = 0, group=None):
         off = 0
         for t in bucket:
             n = t.numel()
-            t.data.copy_(flat[off:off + n].view_as(t))
+            t.copy_(flat[off:off + n].view_as(t))   # bumps _version: device weight caches re-upload
             off += n
         bucket, size = [], 0
 
@@ -139,6 +139,8 @@ def sharded_samples(sample_fn, B: int, group=None):
     """Sample-sharded generation: sample_fn(start, count) -> (count, ...) on each
     rank; returns the full (B, ...) batch on every rank (all-gather)."""
     rank, g = (dist.get_rank(group), dist.get_world_size(group)) if dist.is_initialized() else (0, 1)
+    if B < g:
+        raise ValueError(f"batch of {B} samples cannot be sharded over {g} ranks (every rank needs >= 1 sample)")
     s, e = shard_range(B, rank, g)
     out = sample_fn(s, e - s)
     if g == 1:

@@ -72,6 +72,15 @@ SRA, SRM1, M1, M2, SIGMA, SQRT_ABP, DIR, SIGMA_DDIM = range(8)
 STEP_DDPM, STEP_DDIM = 0, 1
 
 
+def fresh_seed(noise, seed):
+    """The Philox key of a single step: the caller's, or (no explicit noise and no
+    seed) a fresh draw from torch's default generator, so independent calls never
+    share their normals."""
+    if seed is None:
+        return 0 if noise is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
+    return int(seed)
+
+
 class _Sched:
     """Device copy of one fp32 coefficient table (owns a cfd_sched handle)."""
 
@@ -191,16 +200,20 @@ class GaussianDiffusion:
         return {"sample": out, "pred_xstart": xs}
 
     def p_sample(self, model, x, t, clip_denoised=True, denoised_fn=None, cond_fn=None, model_kwargs=None,
-                 noise=None, seed=0, counter=0):
-        """gaussian_diffusion.py:395-439 (noise: explicit normals, else Philox(seed, counter))."""
+                 noise=None, seed=None, counter=0):
+        """gaussian_diffusion.py:395-439 (noise: explicit normals, else Philox(seed, counter);
+        with neither, a fresh seed per call from torch's generator, like the
+        reference's fresh ``randn_like`` at :430)."""
+        seed = fresh_seed(noise, seed)
         t = t.to(device=x.device, dtype=torch.int64).contiguous()
         with torch.no_grad():
             return self._step(STEP_DDPM, model, x, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, noise,
                               seed, counter, 0.0)
 
     def ddim_sample(self, model, x, t, clip_denoised=True, denoised_fn=None, cond_fn=None, model_kwargs=None,
-                    eta=0.0, noise=None, seed=0, counter=0):
-        """gaussian_diffusion.py:537-585."""
+                    eta=0.0, noise=None, seed=None, counter=0):
+        """gaussian_diffusion.py:537-585 (noise / seed as p_sample)."""
+        seed = fresh_seed(noise, seed)
         t = t.to(device=x.device, dtype=torch.int64).contiguous()
         with torch.no_grad():
             return self._step(STEP_DDIM, model, x, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, noise,

@@ -37,7 +37,7 @@ import functools
 import torch
 
 from .. import _lib
-from ..gaussian_diffusion import (LossType, ModelMeanType, ModelVarType, STEP_DDIM, STEP_DDPM,
+from ..gaussian_diffusion import (LossType, ModelMeanType, ModelVarType, STEP_DDIM, STEP_DDPM, fresh_seed,
                                   get_named_beta_schedule)
 from ..respace import SpacedDiffusion, space_timesteps
 from .condition_methods import Identity, PosteriorSampling
@@ -126,12 +126,14 @@ class _GuidedSampler(SpacedDiffusion):
             x = self._guided_step(model, x, i, measurement, method, nz, seed, k, sample_offset, self.distances[k])[0]
         return x
 
-    def p_sample_step(self, model, x, index, measurement, measurement_cond_fn, noise=None, seed=0, counter=0,
+    def p_sample_step(self, model, x, index, measurement, measurement_cond_fn, noise=None, seed=None, counter=0,
                       sample_offset=0):
         """One guided reverse step at respaced index ``index`` (p_sample + conditioning,
         gaussian_diffusion.py:188-199).  Returns dict(sample, pred_xstart, x_t, distance):
-        the conditioned image, x0_hat, the unconditioned DDPM/DDIM sample, the norms."""
+        the conditioned image, x0_hat, the unconditioned DDPM/DDIM sample, the norms.
+        Without ``noise`` and ``seed`` the step draws a fresh Philox key (fresh_seed)."""
         method = _method_of(measurement_cond_fn)
+        seed = fresh_seed(noise, seed)
         x = x.detach().to(torch.float32).contiguous().clone()
         dist = torch.zeros(x.shape[0], dtype=torch.float32, device=x.device)
         img, x0, sample = self._guided_step(model, x, index, measurement, method, noise, seed, counter,

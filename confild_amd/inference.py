@@ -9,6 +9,10 @@ reference-preserving defaults:
   sampler: ddpm | ddim        (reference: ddpm, p_sample_loop)
   coords_path: null           (reference: the CNF trainer's training points)
   seed: 42                    (reference: torch.manual_seed(42), inference.py:17)
+  precision: fp32 | bf16      (reference: fp32.  fp32 runs the U-Net convolutions as
+                               split-f16, fp32-level error; bf16 = config E, bf16
+                               operands with fp32 accumulation, GroupNorm/softmax fp32)
+  compute: split_f16 | fp32 | bf16   (explicit U-Net compute mode; overrides precision)
 Known deviation (fixed on purpose): ``channel_mult`` from the YAML IS passed to
 create_model (the reference reads but drops it, inference.py:38-44, so its own
 case4.yml raises ValueError).
@@ -46,6 +50,20 @@ def latent_denorm(gen: torch.Tensor, vmax: torch.Tensor, vmin: torch.Tensor) -> 
     return out
 
 
+PRECISIONS = {"fp32": "split_f16", "float32": "split_f16", "bf16": "bf16", "bfloat16": "bf16"}
+
+
+def unet_compute(inp) -> str:
+    """U-Net compute mode from the optional ``compute`` / ``precision`` YAML keys."""
+    explicit = getattr(inp, "compute", None)
+    if explicit is not None:
+        return str(explicit)
+    prec = str(getattr(inp, "precision", "fp32")).lower()
+    if prec not in PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {prec!r}")
+    return PRECISIONS[prec]
+
+
 def run(yaml_path: str):
     rank, world, device = dist.init_from_env()
     if device.type != "cuda":
@@ -63,6 +81,7 @@ def run(yaml_path: str):
                          num_head_channels=inp.num_head_channels,
                          attention_resolutions=inp.attention_resolutions,
                          channel_mult=getattr(inp, "channel_mult", None))
+    model.set_compute(unet_compute(inp))
     if rank == 0:
         model.load_state_dict(torch.load(inp.ema_path, weights_only=True, map_location="cpu"))
     model.to(device)
@@ -88,21 +107,25 @@ def run(yaml_path: str):
     coord = cnf.train_coord
     if getattr(inp, "coords_path", None):
         coord = torch.as_tensor(np.load(inp.coords_path), dtype=torch.float32)
-    coord = coord.to(device).reshape(-1, coord.shape[-1])
+    # lumped (N, d) points, or an (h, w, d) grid: the reference keeps the grid
+    # shape and saves (B*T, h, w, c) (train.py:274-277, inference.py:75-81)
+    coord = coord.to(device)
+    spatial = tuple(coord.shape[:-1])
+    npts = int(np.prod(spatial))
     lat = gen.reshape(B * T, L)
     # rows per launch bounded by ~2 GiB of output
-    rows = max(1, (2 << 30) // (coord.shape[0] * cnf.nf.out_features * 4))
+    rows = max(1, (2 << 30) // (npts * cnf.nf.out_features * 4))
     fields = []
     s, e = dist.shard_range(B * T, rank, world)
     for a in range(s, e, rows):
         fields.append(cnf.infer(coord, lat[a:min(e, a + rows)]))
-    local = torch.cat(fields) if fields else torch.empty(0, coord.shape[0], cnf.nf.out_features, device=device)
+    local = torch.cat(fields) if fields else torch.empty((0,) + spatial + (cnf.nf.out_features,), device=device)
     if world > 1:   # gather the decoded fields to rank 0 over RCCL
         sizes = [dist.shard_range(B * T, r, world)[1] - dist.shard_range(B * T, r, world)[0] for r in range(world)]
         local = dist.gather_cat(local, 0, sizes, dst=0)
     if rank == 0:
         out = local.cpu().numpy()
-        np.save(inp.save_path, out)                          # (B*T, N, c), inference.py:79-81
+        np.save(inp.save_path, out)                          # (B*T, N, c) or (B*T, h, w, c), inference.py:79-81
         return out
     return None
 

@@ -1,0 +1,72 @@
+"""Shared definitions of the config-shape golden cases (make_golden_cfg.py writes
+them by running the reference; tests/test_gpu_cfg.py replays them on the HIP
+path).  Nothing here imports the reference: every weight, input, noise draw and
+on-disk file is regenerated from ``confild_amd.synth`` seeds, so only outputs are
+stored in the fixtures."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from confild_amd import synth
+
+# config B (BASELINE.json configs[1]): Case4 uncond U-Net 64^2, DDPM respaced "256"
+TRAJ_B = dict(tag="trajB", seed=1234, B=1, image_size=64, respacing="256",
+              unet=dict(image_size=64, num_channels=128, num_res_blocks=2, channel_mult=None, num_heads=4,
+                        num_head_channels=64, attention_resolutions="32,16,8"),
+              checkpoints=(0, 1, 2, 4, 8, 16, 32, 64, 128, 192, 240, 250, 254, 255))
+
+# config A (configs[0]): Case1 uncond 32^2 mult (1,2,3,4), DDIM-50, 1k-coord decode
+CFG_A = dict(tag="cfgA", seed=1234, image_size=32, respacing="ddim50", vmax=1.5, vmin=-1.5,
+             unet=dict(image_size=32, num_channels=128, num_res_blocks=2, channel_mult="1,2,3,4", num_heads=4,
+                       num_head_channels=64, attention_resolutions="32,16,8"),
+             siren=(2, 32, 3, 10, 128), siren_seed=1234, N=1000)
+
+# config D (configs[3]) widths: DPS with the config-B U-Net and SIREN(3, 64, 3, 15, 384), 10 sensors
+DPS_D = dict(tag="dpsD", seed=1234, respacing="256", scale=1.0, Ns=10, indices=(200, 37, 0),
+             unet=dict(image_size=64, num_channels=128, num_res_blocks=2, channel_mult="", num_heads=4,
+                       num_head_channels=64, attention_resolutions="32,16,8"),
+             siren=(3, 64, 3, 15, 384), siren_seed=4321)
+
+# the real Case4 notebook (inference_phy_random_sensor.ipynb cells 11-20): 384^2 latent,
+# channel_mult "1, 1, 2, 2, 4, 4", the Case4 operator's SIREN(3, 384, 3, 15, 384), 10 sensors
+CASE4_OP = dict(seed=77, T=384, L=384, Ns=10, batch_size=384, siren_seed=4242, unet_seed=1234, dps_index=500,
+                unet=dict(image_size=384, num_channels=128, num_res_blocks=2, channel_mult="1, 1, 2, 2, 4, 4",
+                          num_heads=4, num_head_channels=64, attention_resolutions="32,16,8"))
+
+
+def noise_for(tag: str, k: int, shape) -> np.ndarray:
+    """The k-th normal tensor a reference run draws (torch.randn_like, in order)."""
+    return synth.normal(7, f"{tag}/noise{k}", tuple(shape))
+
+
+def unet_weights(state_dict_or_shapes, seed: int) -> dict:
+    shapes = {k: tuple(v.shape) if hasattr(v, "shape") else tuple(v) for k, v in state_dict_or_shapes.items()}
+    return synth.unet_state_dict(seed, shapes)
+
+
+def case4_files(tmp: str) -> dict:
+    """The on-disk inputs of Case4Operator.__init__ (measurements.py:184-217), from
+    synth seeds: coords.npy, data_max/min.npy, a normaliser file with the
+    x_normalizer_params / y_normalizer0u_params / y_normalizer0l_params keys (the
+    y bounds carry more channels than the 3 the operator keeps), and
+    checkpoint_20000.pt with the hard-coded SIREN(3, 384, 3, 15, 384)."""
+    c = CASE4_OP
+    s = c["siren_seed"]
+    paths = {k: os.path.join(tmp, v) for k, v in dict(coords="coords.npy", max="data_max.npy", min="data_min.npy",
+                                                       normalizer="normalizer_params.pt",
+                                                       ckpt="checkpoint_20000.pt").items()}
+    np.save(paths["coords"], synth.uniform(s, "case4/sensors", (c["Ns"], 3), -0.5, 2.0))
+    np.save(paths["max"], synth.uniform(s, "case4/vmax", (c["L"],), 1.0, 2.0))
+    np.save(paths["min"], -synth.uniform(s, "case4/vmin", (c["L"],), 1.0, 2.0))
+    T = torch.from_numpy
+    xhi, xlo = synth.uniform(s, "case4/xhi", (1, 3), 2.0, 2.5), synth.uniform(s, "case4/xlo", (1, 3), -1.0, -0.5)
+    y0u = (T(synth.uniform(s, "case4/y0u_hi", (5,), 0.5, 2.0)), T(synth.uniform(s, "case4/y0u_lo", (5,), -9., -8.)))
+    y0l = (T(synth.uniform(s, "case4/y0l_hi", (5,), 8.0, 9.0)), T(-synth.uniform(s, "case4/y0l_lo", (5,), 0.5, 2.)))
+    torch.save({"x_normalizer_params": (T(xhi), T(xlo)), "y_normalizer0u_params": y0u,
+                "y_normalizer0l_params": y0l}, paths["normalizer"])
+    sd = synth.siren_state_dict(s, 3, 384, 3, 15, 384)
+    torch.save({"epoch": 20000, "model_state_dict": {k: T(v) for k, v in sd.items()}}, paths["ckpt"])
+    return paths

@@ -119,3 +119,30 @@ def test_bucketed_weight_broadcast():
 def test_gather_to_root_uneven():
     out = _run(_case_gather)
     assert out[0] == [float(i) for i in range(9)] and out[1] is None
+
+
+def _case_broadcast_bumps_version(rank, world):
+    """Cached device weights are keyed on (data_ptr, _version): the broadcast must
+    bump _version so a handle uploaded before it re-uploads."""
+    torch.manual_seed(200 + rank)
+    m = torch.nn.Linear(4, 4)
+    before = [p._version for p in m.parameters()]
+    cdist.broadcast_module(m, src=0)
+    after = [p._version for p in m.parameters()]
+    return all(a > b for a, b in zip(after, before))
+
+
+def _case_too_few_samples(rank, world):
+    try:
+        cdist.sharded_samples(lambda s, c: torch.zeros(c, 2), world - 1)
+    except ValueError:
+        return "ValueError"
+    return "no error"
+
+
+def test_broadcast_bumps_parameter_version():
+    assert _run(_case_broadcast_bumps_version) == {0: True, 1: True}
+
+
+def test_sharded_samples_rejects_batch_below_world():
+    assert _run(_case_too_few_samples) == {0: "ValueError", 1: "ValueError"}

@@ -1,0 +1,204 @@
+"""GPU parity at the BASELINE.json configuration shapes, against fixtures made by
+running the reference (tests/golden/make_golden_cfg.py).  Weights, inputs,
+noise and the Case4 operator's files are regenerated from synth seeds
+(tests/golden/cfg_cases.py); only the reference's outputs are stored.
+
+Stated tolerances, all relative to max(1, max|ref|); the values measured on
+MI355X (round 2) are in brackets and in DESIGN.md section 5:
+  * config B, the full 256-step DDPM loop at B = 1 with the reference's noise:
+    every checkpoint sample and the final latent <= 1e-5 [max 1.3e-6, final
+    1.3e-6]; x0_hat <= 5e-4 [1.5e-4 at step 1, where sqrt(1/abar - 1) ~ 1e2
+    multiplies the eps rounding; 1.3e-6 at the end].  The loop re-injects noise
+    and clamps x0, so the drift does not grow chaotically over the 256 steps;
+  * config A, DDIM-50 + de-normalisation + 1000-coordinate decode of the 32
+    rows: latent <= 1e-4 [1.9e-5: DDIM has no noise to wash out rounding],
+    fields <= 5e-5 [4.8e-6], the decoder alone on the reference's latents
+    <= 2e-5 [6.4e-7];
+  * config D widths, DPS steps at indices 200, 37, 0 from the same state:
+    x0_hat, the DDPM sample and the conditioned image <= 2e-5 [4.2e-6], the
+    residual norm <= 1e-5 relative [1.2e-7];
+  * real Case4 (384^2 U-Net, 108 M parameters, operator from files): operator
+    forward <= 2e-5 [6.0e-7], one DPS step at index 500 <= 2e-5 [x0 2.5e-6,
+    image 3.6e-7, norm 1.6e-7].
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+from confild_amd import synth
+from confild_amd.nf_networks import SIRENAutodecoder_film
+from confild_amd.normalize import Normalizer_ts
+from confild_amd.script_util import create_gaussian_diffusion, create_model
+
+sys.path.insert(0, GOLDEN)
+from cfg_cases import CASE4_OP, CFG_A, DPS_D, TRAJ_B, case4_files, noise_for, unet_weights  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _rel(a, ref):
+    a = a.detach().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    return float(np.abs(a - ref).max()) / max(1.0, float(np.abs(ref).max()))
+
+
+def _unet(case, factory=create_model):
+    m = factory(**case["unet"])
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in unet_weights(m.state_dict(), case["seed"]).items()})
+    return m.to(DEV)
+
+
+def _noise_list(tag, n, shape):
+    return [torch.from_numpy(noise_for(tag, k, shape)).to(DEV) for k in range(n)]
+
+
+def test_configB_full_256_step_trajectory(hip):
+    c = TRAJ_B
+    g = golden("golden_trajB.npz")
+    m = _unet(c)
+    d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=c["respacing"])
+    assert np.array_equal(np.asarray(d.timestep_map), g["timestep_map"])
+    shape = (c["B"], 1, c["image_size"], c["image_size"])
+    x_T = torch.from_numpy(noise_for(c["tag"] + "/xT", 0, shape)).to(DEV)
+    errs = {}
+    cks = [int(k) for k in g["checkpoints"]]
+    for k, out in enumerate(d.p_sample_loop_progressive(m, shape, noise=x_T,
+                                                        step_noise=_noise_list(c["tag"], d.num_timesteps, shape))):
+        if k in cks:
+            j = cks.index(k)
+            errs[k] = (_rel(out["sample"], g["samples"][j]), _rel(out["pred_xstart"], g["pred_xstart"][j]))
+        final = out["sample"]
+    errs["final"] = _rel(final, g["final"])
+    print("config-B trajectory drift (sample, x0) per checkpoint:", errs)
+    assert errs["final"] <= 1e-5, errs
+    assert max(v[0] for k, v in errs.items() if k != "final") <= 1e-5, errs
+    assert max(v[1] for k, v in errs.items() if k != "final") <= 5e-4, errs
+
+
+def test_configA_ddim50_and_decode_end_to_end(hip):
+    from confild_amd.inference import latent_denorm
+    c = CFG_A
+    g = golden("golden_cfgA.npz")
+    m = _unet(c)
+    d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=c["respacing"])
+    assert np.array_equal(np.asarray(d.timestep_map), g["timestep_map"])
+    S = c["image_size"]
+    shape = (1, 1, S, S)
+    x_T = torch.from_numpy(noise_for(c["tag"] + "/xT", 0, shape)).to(DEV)
+    gen = d.ddim_sample_loop(m, shape, noise=x_T, eta=0.0,
+                             step_noise=_noise_list(c["tag"], d.num_timesteps, shape))[:, 0]
+    e_lat = _rel(gen, g["latent"])
+    lat = latent_denorm(gen.contiguous(), torch.full((1,), c["vmax"], device=DEV),
+                        torch.full((1,), c["vmin"], device=DEV))
+    e_den = _rel(lat, g["latent_denorm"])
+    dd, L, co, nh, H = c["siren"]
+    nf = SIRENAutodecoder_film(dd, L, co, nh, H)
+    nf.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(c["siren_seed"], dd, L, co, nh,
+                                                                                   H).items()})
+    nf.to(DEV)
+    xn = Normalizer_ts(params=(torch.ones(1, dd), torch.zeros(1, dd)), method="-11", dim=0)
+    yn = Normalizer_ts(params=(torch.from_numpy(g["ymax"]), torch.from_numpy(g["ymin"])), method="-11", dim=0)
+    fields = nf.decode(torch.from_numpy(g["coords"]).to(DEV), lat.reshape(-1, L)[:, None], xn, yn)
+    e_f = _rel(fields, g["fields"])
+    # the decoder alone, on the reference's own latents (isolates the CNF error)
+    f_ref_lat = nf.decode(torch.from_numpy(g["coords"]).to(DEV),
+                          torch.from_numpy(g["latent_denorm"]).reshape(-1, L)[:, None].to(DEV), xn, yn)
+    e_dec = _rel(f_ref_lat, g["fields"])
+    print(f"config A: latent {e_lat:.2e}, denorm {e_den:.2e}, fields {e_f:.2e}, decoder alone {e_dec:.2e}")
+    assert e_lat <= 1e-4 and e_den <= 1e-4
+    assert e_dec <= 2e-5
+    assert e_f <= 5e-5
+
+
+def _operator_D(g):
+    from confild_amd.guided.measurements import Case4Operator
+    c = DPS_D
+    dd, L, co, nh, H = c["siren"]
+    nf = SIRENAutodecoder_film(dd, L, co, nh, H)
+    nf.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(c["siren_seed"], dd, L, co, nh,
+                                                                                   H).items()})
+    T = lambda k: torch.from_numpy(g[k])  # noqa: E731
+    return Case4Operator.from_parts(DEV, T("coords"), Normalizer_ts(params=(T("xhi"), T("xlo")), method="-11", dim=0),
+                                    Normalizer_ts(params=(T("yhi"), T("ylo")), method="-11", dim=0), nf, T("vmax"),
+                                    T("vmin"), batch_size=16)
+
+
+def _guided(respacing, op, scale):
+    from confild_amd.guided.condition_methods import get_conditioning_method
+    from confild_amd.guided.gaussian_diffusion import create_sampler
+    from confild_amd.guided.measurements import get_noise
+    cond = get_conditioning_method(operator=op, noiser=get_noise(sigma=0.0, name="gaussian"), name="ps", scale=scale)
+    sampler = create_sampler(sampler="ddpm", steps=1000, noise_schedule="cosine", model_mean_type="epsilon",
+                             model_var_type="fixed_large", dynamic_threshold=False, clip_denoised=True,
+                             rescale_timesteps=False, timestep_respacing=respacing)
+    return cond, sampler
+
+
+def test_configD_dps_steps_at_config_widths(hip):
+    from confild_amd.guided.unet import create_model as guided_model
+    c = DPS_D
+    g = golden("golden_dpsD.npz")
+    model = _unet(c, guided_model)
+    op = _operator_D(g)
+    cond, sampler = _guided(c["respacing"], op, c["scale"])
+    y = torch.from_numpy(g["measurement"]).to(DEV)
+    S, L = c["unet"]["image_size"], c["siren"][1]
+    for j, idx in enumerate(c["indices"]):
+        x = torch.from_numpy(synth.normal(c["siren_seed"], f"dpsD/x{idx}", (1, 1, S, L))).to(DEV)
+        nz = torch.from_numpy(noise_for(f"{c['tag']}/{idx}", 0, (1, 1, S, L)))   # p_sample's randn_like
+        out = sampler.p_sample_step(model, x, idx, y, cond.conditioning, noise=nz)
+        e = {k: _rel(out[k], g[f"{r}{j}"]) for k, r in (("pred_xstart", "x0"), ("x_t", "sample"), ("sample", "img"))}
+        ed = abs(float(out["distance"][0]) - float(g[f"dist{j}"])) / float(g[f"dist{j}"])
+        print(f"config D step {idx}: {e}, norm rel {ed:.2e}")
+        assert max(e.values()) <= 2e-5 and ed <= 1e-5, (idx, e, ed)
+
+
+def _case4_operator(tmp):
+    from confild_amd.guided.measurements import get_operator
+    paths = case4_files(str(tmp))
+    return get_operator(device=DEV, name="case4", coords_path=paths["coords"], max_val_path=paths["max"],
+                        min_val_path=paths["min"], normalizer_params_path=paths["normalizer"],
+                        ckpt_path=paths["ckpt"], batch_size=CASE4_OP["batch_size"])
+
+
+def test_case4_operator_from_files(hip, tmp_path):
+    c = CASE4_OP
+    g = golden("golden_case4op.npz")
+    op = _case4_operator(tmp_path)
+    x = torch.from_numpy(synth.uniform(c["seed"], "case4op/x", (1, 1, c["T"], c["L"]), -0.95, 0.95)).to(DEV)
+    A = op.forward(x)
+    err = _rel(A, g["A"])
+    print(f"Case4 operator (files, SIREN(3,384,3,15,384), 10 sensors): {err:.2e}")
+    assert A.shape == g["A"].shape and err <= 2e-5
+
+
+def test_case4_real_shape_dps_step(hip, tmp_path):
+    """The notebook's 384^2 U-Net (channel_mult 1,1,2,2,4,4) loaded from an ema
+    file by create_model(model_path=...), the file-built operator, one DDPM+'ps'
+    step at index 500 of 1000, against the reference's own step."""
+    from confild_amd.guided.unet import create_model as guided_model
+    c = CASE4_OP
+    g = golden("golden_case4dps.npz")
+    op = _case4_operator(tmp_path)
+    kw = c["unet"]
+    shapes = {k: tuple(v.shape) for k, v in guided_model(**kw).state_dict().items()}
+    assert sum(int(np.prod(s)) for s in shapes.values()) == int(g["nparams"])
+    ema = tmp_path / "ema_0.9999_400000.pt"
+    torch.save({k: torch.from_numpy(v) for k, v in synth.unet_state_dict(c["unet_seed"], shapes).items()}, ema)
+    model = guided_model(**kw, model_path=str(ema)).to(DEV)
+    y = torch.from_numpy(golden("golden_case4op.npz")["A"]).to(DEV)   # the reference's measurement of x_true
+    cond, sampler = _guided("", op, 1.0)
+    idx = int(g["index"])
+    x = torch.from_numpy(synth.normal(c["seed"], f"case4dps/x{idx}", (1, 1, c["T"], c["L"]))).to(DEV)
+    nz = torch.from_numpy(noise_for(f"case4dps/{idx}", 0, (1, 1, c["T"], c["L"])))
+    out = sampler.p_sample_step(model, x, idx, y, cond.conditioning, noise=nz)
+    e_x0 = _rel(out["pred_xstart"], g["x0"])
+    e_img = _rel(out["sample"], g["img"])
+    ed = abs(float(out["distance"][0]) - float(g["dist"])) / float(g["dist"])
+    print(f"Case4 384^2 DPS step {idx}: x0 {e_x0:.2e}, img {e_img:.2e}, norm {ed:.2e}")
+    assert e_x0 <= 2e-5 and e_img <= 2e-5 and ed <= 1e-5
+    os.remove(ema)

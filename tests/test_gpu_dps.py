@@ -116,7 +116,7 @@ def _dps_setup(name):
     from confild_amd.guided.unet import create_model as guided_model
     g = golden(f"{name}.npz")
     kw = ast.literal_eval(str(g["kwargs"]))
-    model = guided_model(**kw)                         # "Randomly initialize", as the reference
+    model = guided_model(**kw)                         # no model_path: random init (weights set below)
     sd = synth.unet_state_dict(int(g["seed"]), {k: tuple(v.shape) for k, v in model.state_dict().items()})
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model.to(DEV)

@@ -54,23 +54,34 @@ def test_sharded_sampling_equals_unsharded(hip):
     assert torch.isfinite(full).all()
 
 
-def test_inference_driver_end_to_end(hip, tmp_path):
+@pytest.mark.parametrize("layout", ["lumped", "grid"])
+def test_inference_driver_end_to_end(hip, tmp_path, layout):
+    """lumped: (N, d) points and a per-point output normaliser, saved (B*T, N, c).
+    grid: an (h, w, 2) coordinate grid (the case2 family's train_coord) and a
+    per-channel normaliser; the reference keeps the grid and saves (B*T, h, w, c)."""
     from confild_amd import inference
     kw, m, sd = _tiny()
     torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, tmp_path / "ema.pt")
-    d, L, c, nh, H = 3, 16, 3, 2, 32
-    N = 300
+    if layout == "lumped":
+        d, L, c, nh, H = 3, 16, 3, 2, 32
+        spatial = (300,)
+        yhi = torch.from_numpy(synth.uniform(5, "yhi", (1, 300, c), 0.5, 2.0))
+    else:
+        d, L, c, nh, H = 2, 16, 3, 2, 32
+        spatial = (12, 10)
+        yhi = torch.from_numpy(synth.uniform(5, "yhi", (1, c), 0.5, 2.0))
+    N = int(np.prod(spatial))
     ssd = synth.siren_state_dict(5, d, L, c, nh, H)
     cnf_dir = tmp_path / "cnf"
     cnf_dir.mkdir()
-    yhi = torch.from_numpy(synth.uniform(5, "yhi", (1, N, c), 0.5, 2.0))
     torch.save({"x_normalizer_params": (torch.ones(1, d), torch.zeros(1, d)),
                 "y_normalizer_params": (yhi, -yhi)}, cnf_dir / "normalizer_params.pt")
     torch.save({"epoch": 1, "model_state_dict": {k: torch.from_numpy(v) for k, v in ssd.items()}},
                cnf_dir / "checkpoint_1.pt")
-    coords = synth.uniform(5, "coords", (N, d), 0.0, 1.0)
+    coords = synth.uniform(5, "coords", spatial + (d,), 0.0, 1.0)
     np.save(tmp_path / "coords.npy", coords)
-    cnf_cfg = {"save_path": str(cnf_dir), "coor_path": str(tmp_path / "coords.npy"), "lumped_latent": True,
+    cnf_cfg = {"save_path": str(cnf_dir), "coor_path": str(tmp_path / "coords.npy"),
+               "lumped_latent": layout == "lumped",
                "normalizer": {"method": "-11", "dim": 0}, "multiGPU": 1, "hidden_size": L, "dims": d,
                "NF": {"name": "SIRENAutodecoder_film", "out_features": c, "num_hidden_layers": nh,
                       "hidden_features": H}}
@@ -87,7 +98,7 @@ def test_inference_driver_end_to_end(hip, tmp_path):
     (tmp_path / "case.yml").write_text(yaml.safe_dump(cfg))
     out = inference.run(str(tmp_path / "case.yml"))
     saved = np.load(tmp_path / "out.npy")
-    assert saved.shape == (2 * 16, N, c) and np.array_equal(saved, out)
+    assert saved.shape == (2 * 16,) + spatial + (c,) and np.array_equal(saved, out)
 
     # same latents through the product path by hand, then the CPU oracle decode
     torch.manual_seed(42)
@@ -95,6 +106,7 @@ def test_inference_driver_end_to_end(hip, tmp_path):
     diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="8")
     lat = diff.p_sample_loop(m, (2, 1, 16, 16), seed=seed)[:, 0]
     lat = ((lat + 1) * (1.5 + 1.5) / 2. - 1.5).reshape(32, 16).cpu()
-    ref = osn.decode({k: torch.from_numpy(v) for k, v in ssd.items()}, torch.from_numpy(coords), lat,
+    ref = osn.decode({k: torch.from_numpy(v) for k, v in ssd.items()}, torch.from_numpy(coords).reshape(N, d), lat,
                      torch.ones(1, d), torch.zeros(1, d), yhi, -yhi)
+    ref = ref.reshape((32,) + spatial + (c,))
     assert np.abs(saved - ref.numpy()).max() <= 2e-5 * max(1.0, float(ref.abs().max()))

@@ -3,7 +3,8 @@ fixtures and the CPU oracle on identical inputs.
 
 Tolerances (fp32 everywhere; the HIP kernels sum in a different order than
 MKL/oneDNN on the CPU):
-  * U-Net forward: max|d| / max|ref| <= 1e-4;
+  * U-Net forward: max|d| / max|ref| <= 1e-5 (measured values are
+    printed and recorded in DESIGN.md section 5);
   * one sampler step given the same eps and noise: bit-exact;
   * short trajectories (8 DDPM / 5 DDIM steps): max|d| <= 1e-4;
   * SIREN/FiLM decode: max|d| <= 2e-5 * max(1, max|ref|) (sin(30 x) amplifies
@@ -43,7 +44,8 @@ def test_unet_forward_vs_reference_golden(hip, name):
     eps = m(torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["t"]).to(DEV)).cpu().numpy()
     ref = g["eps"]
     err = np.abs(eps - ref).max() / np.abs(ref).max()
-    assert err <= 1e-4, err
+    print(f"U-Net {name} vs reference: {err:.2e}")
+    assert err <= 1e-5, err
 
 
 def test_unet_batch_vs_oracle_cfgB(hip):
@@ -55,7 +57,8 @@ def test_unet_batch_vs_oracle_cfgB(hip):
     with torch.no_grad():
         ref = ou.forward(sd, ou.Config(**kw), x, t)
     err = (eps - ref).abs().max().item() / ref.abs().max().item()
-    assert err <= 1e-4, err
+    print(f"U-Net cfgB64 B=3 vs oracle: {err:.2e}")
+    assert err <= 1e-5, err
     # batch independence: sample 1 alone equals sample 1 in the batch
     e1 = m(x[1:2].to(DEV), t[1:2].to(DEV)).cpu()
     assert (e1 - eps[1:2]).abs().max().item() <= 1e-5 * ref.abs().max().item()

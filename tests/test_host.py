@@ -149,3 +149,47 @@ def test_trainer_loads_reference_files(tmp_path):
         cfg["save_path"] = str(tmp_path / "missing")
         (tmp_path / "d.yml").write_text(yaml.safe_dump(cfg))
         trainer(basic_input(str(tmp_path / "d.yml")), infer_mode=True)
+
+
+def test_inference_precision_key():
+    """inference.py's optional precision / compute YAML keys (config E reachable
+    through the drop-in driver)."""
+    from types import SimpleNamespace as NS
+    from confild_amd.inference import unet_compute
+    assert unet_compute(NS()) == "split_f16"
+    assert unet_compute(NS(precision="fp32")) == "split_f16"
+    assert unet_compute(NS(precision="bf16")) == "bf16"
+    assert unet_compute(NS(precision="bf16", compute="fp32")) == "fp32"
+    with pytest.raises(ValueError):
+        unet_compute(NS(precision="fp16"))
+
+
+def test_guided_create_model_fails_loudly(tmp_path):
+    """a bad checkpoint raises (the reference silently random-inits,
+    C/unet.py:86-90; random_init_on_error=True keeps that behaviour)."""
+    from confild_amd.guided.unet import create_model as gcm
+    kw = dict(image_size=16, num_channels=32, num_res_blocks=1, channel_mult="1,2", num_heads=4,
+              num_head_channels=16, attention_resolutions="8")
+    with pytest.raises(RuntimeError):
+        gcm(**kw, model_path=str(tmp_path / "missing.pt"))
+    torch.save({"bogus": torch.zeros(1)}, tmp_path / "bad.pt")
+    with pytest.raises(RuntimeError):
+        gcm(**kw, model_path=str(tmp_path / "bad.pt"))
+    m = gcm(**kw, model_path=str(tmp_path / "bad.pt"), random_init_on_error=True)
+    good = {k: v.clone() + 1 for k, v in m.state_dict().items()}
+    torch.save(good, tmp_path / "good.pt")
+    m2 = gcm(**kw, model_path=str(tmp_path / "good.pt"))
+    assert all(torch.equal(m2.state_dict()[k], v) for k, v in good.items())
+    with pytest.warns(UserWarning):
+        gcm(**kw)
+
+
+def test_single_step_default_noise_is_fresh():
+    """p_sample / ddim_sample without noise or seed draw a fresh Philox key per call
+    (the reference draws a fresh randn_like per call, gaussian_diffusion.py:430)."""
+    torch.manual_seed(0)
+    a = gd.fresh_seed(None, None)
+    b = gd.fresh_seed(None, None)
+    assert a != b
+    assert gd.fresh_seed(torch.zeros(1), None) == 0
+    assert gd.fresh_seed(None, 7) == 7

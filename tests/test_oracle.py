@@ -154,3 +154,109 @@ def test_dps_loop_matches_reference(name):
         assert np.abs(img.numpy() - g["img"][k]).max() < 2e-5 * scale, k
         assert abs(float(norm) - g["dist"][k]) < 1e-5 * max(1.0, g["dist"][k]), k
     assert np.abs(traj[-1][0].numpy() - g["out"]).max() < 2e-5 * max(1.0, float(np.abs(g["out"]).max()))
+
+
+# ---------------------------------------------------------------------------
+# config-shape fixtures (tests/golden/make_golden_cfg.py): the oracle against
+# the reference at the BASELINE.json widths, at CPU-affordable lengths
+# ---------------------------------------------------------------------------
+def _cfg_cases():
+    import sys
+    from conftest import GOLDEN
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    import cfg_cases
+    return cfg_cases
+
+
+def test_oracle_configB_trajectory_prefix():
+    """First 8 of the 256 DDPM steps of config B (the full loop is the GPU test)."""
+    cc = _cfg_cases()
+    c = cc.TRAJ_B
+    g = golden("golden_trajB.npz")
+    cfg = ou.Config(**c["unet"])
+    sd = {k: torch.from_numpy(v) for k, v in cc.unet_weights(ou.param_shapes(cfg), c["seed"]).items()}
+    tb = od.Tables(1000, "cosine", c["respacing"])
+    shape = (c["B"], 1, c["image_size"], c["image_size"])
+    x = torch.from_numpy(cc.noise_for(c["tag"] + "/xT", 0, shape))
+    cks = [int(k) for k in g["checkpoints"]]
+    with torch.no_grad():
+        for k, i in enumerate(reversed(range(tb.num_timesteps))):
+            if k > 8:
+                break
+            t = torch.full((c["B"],), i, dtype=torch.int64)
+            eps = ou.forward(sd, cfg, x, torch.from_numpy(tb.timestep_map)[t])
+            x, x0 = od.ddpm_step(tb, x, t, eps, torch.from_numpy(cc.noise_for(c["tag"], k, shape)))
+            if k in cks:
+                j = cks.index(k)
+                assert np.abs(x.numpy() - g["samples"][j]).max() < 2e-5, k
+                assert np.abs(x0.numpy() - g["pred_xstart"][j]).max() < 2e-5, k
+
+
+def test_oracle_configA_end_to_end():
+    cc = _cfg_cases()
+    c = cc.CFG_A
+    g = golden("golden_cfgA.npz")
+    cfg = ou.Config(**c["unet"])
+    sd = {k: torch.from_numpy(v) for k, v in cc.unet_weights(ou.param_shapes(cfg), c["seed"]).items()}
+    tb = od.Tables(1000, "cosine", c["respacing"])
+    assert np.array_equal(tb.timestep_map, g["timestep_map"])
+    S = c["image_size"]
+    x = torch.from_numpy(cc.noise_for(c["tag"] + "/xT", 0, (1, 1, S, S)))
+    with torch.no_grad():
+        for k, i in enumerate(reversed(range(tb.num_timesteps))):
+            t = torch.full((1,), i, dtype=torch.int64)
+            eps = ou.forward(sd, cfg, x, torch.from_numpy(tb.timestep_map)[t])
+            x, _ = od.ddim_step(tb, x, t, eps, torch.from_numpy(cc.noise_for(c["tag"], k, (1, 1, S, S))))
+    assert np.abs(x[:, 0].numpy() - g["latent"]).max() < 1e-4
+    d, L, co, nh, H = c["siren"]
+    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(c["siren_seed"], d, L, co, nh, H).items()}
+    T = torch.from_numpy
+    with torch.no_grad():
+        f = osn.decode(ssd, T(g["coords"]), T(g["latent_denorm"]).reshape(-1, L), torch.ones(1, d),
+                       torch.zeros(1, d), T(g["ymax"]), T(g["ymin"]))
+    assert np.abs(f.numpy() - g["fields"]).max() < 2e-5 * max(1.0, float(np.abs(g["fields"]).max()))
+
+
+def test_oracle_configD_dps_steps():
+    cc = _cfg_cases()
+    c = cc.DPS_D
+    g = golden("golden_dpsD.npz")
+    cfg = ou.Config(**c["unet"])
+    sd = {k: torch.from_numpy(v) for k, v in cc.unet_weights(ou.param_shapes(cfg), c["seed"]).items()}
+    d, L, co, nh, H = c["siren"]
+    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(c["siren_seed"], d, L, co, nh, H).items()}
+    T = lambda k: torch.from_numpy(g[k])  # noqa: E731
+    operator = lambda x0: odps.case4_forward(ssd, T("coords"), T("xhi"), T("xlo"), T("yhi"), T("ylo"),  # noqa: E731
+                                             T("vmax"), T("vmin"), x0, batch=16)
+    unet = lambda x, t: ou.forward(sd, cfg, x, t)  # noqa: E731
+    tb = od.Tables(1000, "cosine", c["respacing"])
+    S = c["unet"]["image_size"]
+    for j, idx in enumerate(c["indices"]):
+        x = torch.from_numpy(synth.normal(c["siren_seed"], f"dpsD/x{idx}", (1, 1, S, L)))
+        nz = torch.from_numpy(cc.noise_for(f"{c['tag']}/{idx}", 0, (1, 1, S, L)))
+        img, x0, sample, norm = odps.dps_step(tb, unet, operator, x, idx, T("measurement"), nz, c["scale"])
+        sc = max(1.0, float(np.abs(g[f"img{j}"]).max()))
+        assert np.abs(x0.numpy() - g[f"x0{j}"]).max() < 2e-5 * sc, idx
+        assert np.abs(sample.numpy() - g[f"sample{j}"]).max() < 2e-5 * sc, idx
+        assert np.abs(img.numpy() - g[f"img{j}"]).max() < 2e-5 * sc, idx
+        assert abs(float(norm) - float(g[f"dist{j}"])) < 1e-5 * float(g[f"dist{j}"]), idx
+
+
+def test_oracle_case4_operator_from_files(tmp_path):
+    """The operator's file formats (measurements.py:184-217) read by the oracle
+    side: y bounds from y_normalizer0u (upper) / y_normalizer0l (lower), first 3."""
+    cc = _cfg_cases()
+    c = cc.CASE4_OP
+    g = golden("golden_case4op.npz")
+    p = cc.case4_files(str(tmp_path))
+    prm = torch.load(p["normalizer"], weights_only=True)
+    ssd = torch.load(p["ckpt"], weights_only=True)["model_state_dict"]
+    xh, xl = prm["x_normalizer_params"]
+    yh, yl = prm["y_normalizer0u_params"][0][:3], prm["y_normalizer0l_params"][1][:3]
+    x = torch.from_numpy(synth.uniform(c["seed"], "case4op/x", (1, 1, c["T"], c["L"]), -0.95, 0.95))
+    with torch.no_grad():
+        A = odps.case4_forward(ssd, torch.from_numpy(np.load(p["coords"])).float(), xh, xl, yh, yl,
+                               torch.from_numpy(np.load(p["max"])), torch.from_numpy(np.load(p["min"])), x,
+                               batch=c["batch_size"])
+    assert np.abs(A.numpy() - g["A"]).max() < 2e-5 * max(1.0, float(np.abs(g["A"]).max()))
