@@ -1,33 +1,41 @@
-"""Benchmark: CoNFiLD Case4 unconditional generation on MI355X.
+"""Benchmark: CoNFiLD generation on MI355X (BASELINE.json metric: generated
+fields/sec, 256-step sample + CNF decode, Case4 latent, 1/2/4/8 GPU).
 
-One step = one batch of the BASELINE.json configs[1] workload on each GPU:
-  * 256-step DDPM reverse loop (cosine-1000 respaced "256", FIXED_LARGE, clip) of
-    the 64x64 latent U-Net (create_model(64, 128 ch, 2 res blocks, attention
-    32,16,8, 64-ch heads): 89.5 M parameters) at batch 8;
+Default (``--config B``): one step = one pass of BASELINE.json configs[1]:
+  * the 256-step DDPM reverse loop (cosine-1000 respaced "256", FIXED_LARGE,
+    clip) of the 64x64 latent U-Net (create_model(64, 128 ch, 2 res blocks,
+    attention 32,16,8, 64-ch heads): 89.5 M parameters);
   * latent de-normalisation (scripts/inference.py:59-61);
-  * CNF decode of all 8 x 64 latent rows with SIRENAutodecoder_film(3, 64, 3, 15,
-    384) on the 64^3 = 262,144-point lattice (normaliser + per-point
-    de-normaliser fused) -> 8 fields of shape (64, 262144, 3) resident in HBM.
-Weights and inputs are synthetic (confild_amd.synth, seed 1234); there is no
-network access for checkpoints.  Multi-GPU: one process per GPU (torchrun), each
-rank generates its own batch of 8 (weak scaling, no data-path collective).
+  * CNF decode of every latent row with SIRENAutodecoder_film(3, 64, 3, 15, 384)
+    on the 64^3 = 262,144-point lattice (normaliser + per-point de-normaliser
+    fused) -> fields of shape (64, 262144, 3) resident in HBM.
 
-Prints ONE JSON line (rank 0) with the driver contract plus a ``roofline`` object
-for the dominant kernel (the CNF decoder, timed with HIP events on its stream) and
-a ``cpu_baseline`` measured on this host's cores with the oracle (rank 0, N=1).
+Multi-GPU (one process per GPU, torchrun, RCCL = the "nccl" backend), the
+north-star design: rank 0 builds the weights and
+broadcasts them once (dist.broadcast_module); samples are sharded with the
+world-size-invariant Philox stream (sample_offset); every rank decodes the rows
+of its own samples; the decoded fields are gathered to rank 0 over xGMI inside
+the timed region (``--no-gather`` keeps them on their ranks).
+  * ``--scaling weak`` (default): 8 samples per GPU (global batch 8 N);
+  * ``--scaling strong``: config B's global batch of 8 split over the ranks
+    (1 sample per GPU at N = 8).
 
-The U-Net convolutions (split_f16 conv_gemm) and the decoder's hidden layers run by
-default as split-f16 (siren_fused_split: three
-f16 MFMAs per fp32 product on 22-bit operand splits, fp32-level error against an
-fp64 evaluation -- tests/test_gpu_siren_split.py); its roofline is the f16 dense
-MFMA peak / 3.  ``--siren-compute f32`` runs the exact fp32 MFMA chain
-(siren_fused) against the fp32 MFMA peak instead.
+``--config C`` (BASELINE.json configs[2]): CNF-only decode of 256 latents x 2^22
+uniform coordinates with the Case4 CNF SIREN(3, 384, 3, 15, 384), coordinates
+sharded over the ranks (dist.sharded_decode's layout), slabs gathered to rank 0.
+
+Weights and inputs are synthetic and seeded (confild_amd.synth); there is no
+network access for checkpoints.  Rank 0 prints ONE JSON line with the driver
+contract, a ``roofline`` object for the dominant kernel (the CNF decoder, HIP
+events on its stream), a ``roofline_unet`` object for the U-Net forward, and a
+``cpu_baseline`` (the oracle on this host's cores, rank 0, N = 1).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -37,14 +45,18 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-B = 8            # samples per GPU
+B = 8            # config B samples per batch
 S = 64           # latent image (T = L = 64)
 STEPS = "256"    # timestep respacing
 GRID = 64        # 64^3 lattice
-CNF = dict(d=3, L=64, c=3, nh=15, H=384)
+CNF_B = dict(d=3, L=64, c=3, nh=15, H=384)
+CNF_C = dict(d=3, L=384, c=3, nh=15, H=384)
+C_COORDS = 1 << 22
+C_LATENTS = 256
 FMA_PEAK_TFLOPS = 157.3    # MI355X fp32 matrix peak (MI355X_MICROARCH.md chip table)
 F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16/bf16 matrix peak (same table; no sparsity)
-HBM_PEAK_GBS = 8000.0
+UNET_FLOPS_PER_SAMPLE = 68.61e9   # config-B U-Net forward, 2*MAC of conv/bmm/addmm (FlopCounter)
+METRIC = "generated fields/sec (256-step sample + CNF decode), Case4 latent, 1/2/4/8 GPU"
 
 # dominant-kernel roofline per decoder compute mode:
 #   (kernel name, peak in algorithmic fp32 TFLOP/s, basis, committed PMC record)
@@ -57,7 +69,8 @@ ROOFLINE = {
 
 def measured_traffic(mode, latents, npts):
     """Per-launch fabric bytes of the decoder kernel from the committed rocprofv3
-    PMC record (tools/pmc_traffic.py), scaled from its launch geometry to this one."""
+    PMC record (tools/pmc_traffic.py), scaled from its launch geometry to this one
+    (valid for the same SIREN widths)."""
     kname, _, _, fname = ROOFLINE[mode]
     try:
         rec = json.load(open(os.path.join(ROOT, "profiles", fname)))
@@ -71,8 +84,8 @@ def measured_traffic(mode, latents, npts):
 
 
 def measured_mfma_util(kname):
-    """Matrix-pipe busy fraction and held clock of the decoder kernel from the
-    committed rocprofv3 record (tools/gpujob_mfma_util.sh, tools/mfma_util.py)."""
+    """Matrix-pipe busy fraction and held clock from the committed rocprofv3 record
+    (tools/gpujob_mfma_util.sh, tools/mfma_util.py)."""
     try:
         rec = json.load(open(os.path.join(ROOT, "profiles", "r01_mfma_util.json")))
     except (OSError, ValueError):
@@ -88,118 +101,10 @@ def siren_flops_per_pair(d, L, c, nh, H):
     return 2 * (d * H + nh * H * H + H * c)
 
 
-def unet_flops_per_sample():
-    # conv/bmm/addmm MAC*2 for the config-B U-Net forward (FlopCounter, torch 2.10)
-    return 68.61e9
-
-
-def setup(dev, siren_compute="split_f16", unet_compute="split_f16"):
-    from confild_amd import synth
-    from confild_amd.nf_networks import SIRENAutodecoder_film
-    from confild_amd.normalize import Normalizer_ts
-    from confild_amd.script_util import create_gaussian_diffusion, create_model
-    model = create_model(image_size=S, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
-                         attention_resolutions="32,16,8")
-    sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in model.state_dict().items()})
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    model.to(dev)
-    model.set_compute(unet_compute)
-    diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=STEPS)
-    c = CNF
-    nf = SIRENAutodecoder_film(c["d"], c["L"], c["c"], c["nh"], c["H"])
-    nf.load_state_dict({k: torch.from_numpy(v) for k, v in
-                        synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"], c["H"]).items()})
-    nf.to(dev)
-    nf.set_compute(siren_compute)
-    ax = torch.linspace(0, 1, GRID)
-    coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3).to(dev)
-    N = coords.shape[0]
-    xn = Normalizer_ts(params=(torch.ones(1, 3, device=dev), torch.zeros(1, 3, device=dev)), method="-11", dim=0)
-    ymax = torch.from_numpy(synth.uniform(9, "ymax", (1, N, 3), 0.5, 2.0)).to(dev)
-    ymin = -torch.from_numpy(synth.uniform(9, "ymin", (1, N, 3), 0.5, 2.0)).to(dev)
-    yn = Normalizer_ts(params=(ymax, ymin), method="-11", dim=0)
-    vmax = torch.full((1,), 1.5, device=dev)
-    vmin = torch.full((1,), -1.5, device=dev)
-    return model, diff, nf, coords, xn, yn, vmax, vmin
-
-
-def generate(objs, dev, seed, ev=None):
-    """One batch: sample -> de-normalise -> decode.  Returns fields (B*T, N, c)."""
-    from confild_amd import _lib
-    model, diff, nf, coords, xn, yn, vmax, vmin = objs
-    lat = diff.p_sample_loop(model, (B, 1, S, S), seed=seed)[:, 0]          # (B, T, L)
-    den = torch.empty_like(lat)
-    _lib.check(_lib.load().cfd_latent_denorm(_lib.ptr(lat), _lib.ptr(den), lat.numel(), _lib.ptr(vmax),
-                                             _lib.ptr(vmin), 1, _lib.stream_of(dev)), "denorm")
-    if ev is not None:
-        ev[0].record()
-    fields = nf.decode(coords, den.reshape(B * S, 1, S), xn, yn)              # (B*T, N, c)
-    if ev is not None:
-        ev[1].record()
-    return fields
-
-
-def cpu_baseline(budget_s=20.0):
-    """Oracle (torch CPU restatement of the reference path) on this host's cores,
-    on a bounded sample; extrapolated to fields/s.  The reference itself never
-    runs on the GPU box."""
-    from confild_amd import synth
-    from oracle import siren as osn
-    from oracle import unet as ou
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    torch.set_num_threads(threads)
-    cfg = ou.Config(image_size=S, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
-                    attention_resolutions="32,16,8")
-    sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(1234, ou.param_shapes(cfg)).items()}
-    x = torch.randn(B, 1, S, S)
-    t = torch.full((B,), 500, dtype=torch.int64)
-    with torch.no_grad():
-        ou.forward(sd, cfg, x[:1], t[:1])  # warm
-        t0 = time.perf_counter()
-        nstep = 0
-        while True:
-            ou.forward(sd, cfg, x, t)
-            nstep += 1
-            if time.perf_counter() - t0 > budget_s / 2 or nstep >= 3:
-                break
-        unet_step = (time.perf_counter() - t0) / nstep
-    c = CNF
-    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"],
-                                                                      c["H"]).items()}
-    npts = 16384
-    coords = torch.rand(npts, 3)
-    lat = torch.randn(2, c["L"])
-    with torch.no_grad():
-        osn.decode(ssd, coords[:1024], lat[:1], torch.ones(1, 3), torch.zeros(1, 3), torch.ones(1, 3),
-                   -torch.ones(1, 3))
-        t0 = time.perf_counter()
-        nd = 0
-        while True:
-            osn.decode(ssd, coords, lat, torch.ones(1, 3), torch.zeros(1, 3), torch.ones(1, 3), -torch.ones(1, 3))
-            nd += 1
-            if time.perf_counter() - t0 > budget_s / 2 or nd >= 4:
-                break
-        pair_s = (time.perf_counter() - t0) / (nd * npts * lat.shape[0])
-    N = GRID ** 3
-    per_field = 256 * unet_step / B + S * N * pair_s
-    return {"value": 1.0 / per_field, "unit": "fields/s", "cores": threads, "kind": "port",
-            "sample": (f"oracle (torch CPU restatement): {nstep} U-Net forwards at B={B} "
-                       f"({unet_step:.3f} s each) + {nd} decodes of {lat.shape[0]} latents x {npts} coords "
-                       f"({pair_s * 1e9:.1f} ns/pair); extrapolated to 256 steps/{B} samples + {S}x{N} pairs "
-                       f"per field")}
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--siren-compute", choices=["split_f16", "f32"], default="split_f16")
-    ap.add_argument("--unet-compute", choices=["split_f16", "fp32"], default="split_f16")
-    args = ap.parse_args()
-
+# ---------------------------------------------------------------------------
+# distributed plumbing
+# ---------------------------------------------------------------------------
+def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -210,67 +115,357 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    objs = setup(dev, args.siren_compute, args.unet_compute)
-    mode = objs[2].compute_mode(dev)
-    kname, peak, peak_basis, _ = ROOFLINE[mode]
+    return rank, world, dev
 
-    def barrier():
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-            torch.cuda.synchronize(dev)
 
-    for w in range(args.warmup):
-        generate(objs, dev, seed=1000 * rank + w)
-    barrier()
-    ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-    dec_ms = []
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        fields = generate(objs, dev, seed=10 ** 6 + 1000 * rank + k, ev=ev)
-        ev[1].synchronize()
-        dec_ms.append(ev[0].elapsed_time(ev[1]))
-    barrier()
-    elapsed = time.perf_counter() - t0
+def barrier(dev, world):
+    torch.cuda.synchronize(dev)
     if world > 1:
         import torch.distributed as dist
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
-    fields_total = B * world * args.steps
-    value = fields_total / elapsed
-    c = CNF
-    pairs = B * S * GRID ** 3
-    flops = pairs * siren_flops_per_pair(**c)
-    dec_s = float(np.mean(dec_ms)) / 1e3
-    achieved = flops / dec_s / 1e12
-    assert torch.isfinite(fields).all().item(), "non-finite output"
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(v, dev, world):
+    if world == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def gather_to_root(x, dim, sizes, world):
+    if world == 1:
+        return x
+    from confild_amd import dist as cdist
+    return cdist.gather_cat(x, dim, sizes, dst=0)
+
+
+# ---------------------------------------------------------------------------
+# config B: sample -> de-normalise -> decode
+# ---------------------------------------------------------------------------
+def setup_B(dev, rank, world, siren_compute, unet_compute):
+    from confild_amd import dist as cdist
+    from confild_amd import synth
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    from confild_amd.normalize import Normalizer_ts
+    from confild_amd.script_util import create_gaussian_diffusion, create_model
+    model = create_model(image_size=S, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                         attention_resolutions="32,16,8")
+    c = CNF_B
+    nf = SIRENAutodecoder_film(c["d"], c["L"], c["c"], c["nh"], c["H"])
+    if rank == 0:   # rank 0 owns the "checkpoint"; the others receive it over RCCL
+        sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in model.state_dict().items()})
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        nf.load_state_dict({k: torch.from_numpy(v) for k, v in
+                            synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"], c["H"]).items()})
+    model.to(dev)
+    nf.to(dev)
+    cdist.broadcast_module(model)
+    cdist.broadcast_module(nf)
+    model.set_compute(unet_compute)
+    nf.set_compute(siren_compute)
+    diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=STEPS)
+    ax = torch.linspace(0, 1, GRID)
+    coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3).to(dev)
+    N = coords.shape[0]
+    xn = Normalizer_ts(params=(torch.ones(1, 3, device=dev), torch.zeros(1, 3, device=dev)), method="-11", dim=0)
+    ymax = torch.from_numpy(synth.uniform(9, "ymax", (1, N, 3), 0.5, 2.0)).to(dev)
+    ymin = -torch.from_numpy(synth.uniform(9, "ymin", (1, N, 3), 0.5, 2.0)).to(dev)
+    yn = Normalizer_ts(params=(ymax, ymin), method="-11", dim=0)
+    vmax = torch.full((1,), 1.5, device=dev)
+    vmin = torch.full((1,), -1.5, device=dev)
+    return dict(model=model, diff=diff, nf=nf, coords=coords, xn=xn, yn=yn, vmax=vmax, vmin=vmin)
+
+
+def step_B(o, dev, seed, start, count, ev=None):
+    """This rank's samples [start, start+count) of one batch: sample -> de-normalise
+    -> decode.  Returns fields (count*T, N, c).  ev: 3 events (U-Net start,
+    decode start, decode end)."""
+    from confild_amd import _lib
+    if ev is not None:
+        ev[0].record()
+    lat = o["diff"].p_sample_loop(o["model"], (count, 1, S, S), seed=seed, sample_offset=start)[:, 0]
+    den = torch.empty_like(lat)
+    _lib.check(_lib.load().cfd_latent_denorm(_lib.ptr(lat), _lib.ptr(den), lat.numel(), _lib.ptr(o["vmax"]),
+                                             _lib.ptr(o["vmin"]), 1, _lib.stream_of(dev)), "denorm")
+    if ev is not None:
+        ev[1].record()
+    fields = o["nf"].decode(o["coords"], den.reshape(count * S, 1, S), o["xn"], o["yn"])
+    if ev is not None:
+        ev[2].record()
+    return fields
+
+
+# ---------------------------------------------------------------------------
+# config C: coordinate-sharded CNF-only decode
+# ---------------------------------------------------------------------------
+def setup_C(dev, rank, world, siren_compute):
+    from confild_amd import dist as cdist
+    from confild_amd import synth
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    from confild_amd.normalize import Normalizer_ts
+    c = CNF_C
+    nf = SIRENAutodecoder_film(c["d"], c["L"], c["c"], c["nh"], c["H"])
+    if rank == 0:
+        nf.load_state_dict({k: torch.from_numpy(v) for k, v in
+                            synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"], c["H"]).items()})
+    nf.to(dev)
+    cdist.broadcast_module(nf)
+    nf.set_compute(siren_compute)
+    coords, lat, ymax, ymin, (s, e) = c_inputs(rank, world, C_COORDS, C_LATENTS, c["L"])
+    lat = lat.to(dev)
+    if world > 1:   # latents travel from rank 0 (the sampler's output in a full pipeline)
+        import torch.distributed as dist
+        dist.broadcast(lat, src=0)
+    xn = Normalizer_ts(params=(torch.ones(1, 3, device=dev), torch.zeros(1, 3, device=dev)), method="-11", dim=0)
+    yn = Normalizer_ts(params=(ymax.to(dev), ymin.to(dev)), method="-11", dim=0)
+    return dict(nf=nf, coords=coords.to(dev), lat=lat[:, None], xn=xn, yn=yn, shard=(s, e))
+
+
+def c_inputs(rank, world, n_coords, n_latents, L):
+    """Config C inputs of one rank: its contiguous coordinate shard with the
+    matching rows of the per-point output normaliser, and all latents.  The
+    counter-based stream makes every shard independent of the rank count."""
+    from confild_amd import dist as cdist
+    from confild_amd import synth
+    s, e = cdist.shard_range(n_coords, rank, world)
+    coords = torch.from_numpy(synth.uniform(7, "C/coords", (n_coords, 3), 0.0, 1.0)[s:e])
+    lat = torch.from_numpy(synth.normal(11, "C/latents", (n_latents, L)) * np.float32(0.5))
+    ymax = torch.from_numpy(synth.uniform(9, "C/ymax", (1, n_coords, 3), 0.5, 2.0)[:, s:e])
+    ymin = -torch.from_numpy(synth.uniform(9, "C/ymin", (1, n_coords, 3), 0.5, 2.0)[:, s:e])
+    return coords, lat, ymax, ymin, (s, e)
+
+
+def b_shards(scaling, world):
+    """Config B sample shards [(start, count)] per rank: 8 per GPU (weak) or the
+    global batch of 8 split (strong)."""
+    from confild_amd import dist as cdist
+    glob = B * world if scaling == "weak" else B
+    if glob < world:
+        raise ValueError(f"strong scaling needs a global batch >= world size ({glob} < {world})")
+    return [(cdist.shard_range(glob, r, world)[0],
+             cdist.shard_range(glob, r, world)[1] - cdist.shard_range(glob, r, world)[0]) for r in range(world)]
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (oracle on this host's cores)
+# ---------------------------------------------------------------------------
+def _cpu_info():
+    model = platform.processor() or "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:   # cgroup v2 CPU share of this process
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    tpc = 1
+    try:
+        sib = open("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list").read().strip()
+        tpc = len([x for part in sib.split(",") for x in
+                   (range(int(part.split("-")[0]), int(part.split("-")[1]) + 1) if "-" in part else [part])])
+    except (OSError, ValueError):
+        pass
+    physical = max(1, aff // tpc)
+    threads = min(physical, quota) if quota else physical
+    return dict(cpu_model=model, affinity_cpus=aff, threads_per_core=tpc, cgroup_cpu_quota=quota), threads
+
+
+def _time_loop(fn, n_min, budget_s):
+    fn()  # warm
+    t0 = time.perf_counter()
+    n = 0
+    while n < n_min or (time.perf_counter() - t0 < budget_s and n < 2 * n_min):
+        fn()
+        n += 1
+    return (time.perf_counter() - t0) / n, n
+
+
+def cpu_baseline(config):
+    """The oracle (torch CPU restatement of the reference path, the same aten ops
+    in the same order) on all physical cores this process may use (SURVEY 8d,
+    BASELINE.md section 3): 8 U-Net sampler steps at B = 8 and one decode chunk
+    of >= 2^20 (coordinate, latent) pairs, measured; fields/s extrapolated
+    linearly (the per-step and per-pair costs are constant)."""
+    from confild_amd import synth
+    from oracle import siren as osn
+    from oracle import unet as ou
+    info, threads = _cpu_info()
+    torch.set_num_threads(threads)
+    out = {"unit": "fields/s", "cores": threads, "kind": "port", "torch": torch.__version__, **info}
+    if config == "B":
+        cfg = ou.Config(image_size=S, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                        attention_resolutions="32,16,8")
+        sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(1234, ou.param_shapes(cfg)).items()}
+        x = torch.randn(B, 1, S, S)
+        t = torch.full((B,), 500, dtype=torch.int64)
+        with torch.no_grad():
+            unet_step, nstep = _time_loop(lambda: ou.forward(sd, cfg, x, t), 8, 0.0)
+        c = CNF_B
+        npts, nl = 65536, 16
+    else:
+        unet_step, nstep = 0.0, 0
+        c = CNF_C
+        npts, nl = 65536, 16
+    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"],
+                                                                      c["H"]).items()}
+    coords = torch.rand(npts, 3)
+    lat = torch.randn(nl, c["L"])
+    one, mone = torch.ones(1, 3), -torch.ones(1, 3)
+    with torch.no_grad():
+        osn.decode(ssd, coords[:1024], lat[:1], one, torch.zeros(1, 3), one, mone)
+        t0 = time.perf_counter()
+        osn.decode(ssd, coords, lat, one, torch.zeros(1, 3), one, mone)
+        dec_s = time.perf_counter() - t0
+    pairs = npts * nl
+    pair_s = dec_s / pairs
+    if config == "B":
+        per_field = 256 * unet_step / B + S * GRID ** 3 * pair_s
+        out["measured"] = {"unet_forward_b8_s": unet_step, "unet_forwards": nstep,
+                           "decode_pairs": pairs, "decode_s": dec_s, "ns_per_pair": pair_s * 1e9}
+        out["extrapolated"] = {"unet_s_per_field": 256 * unet_step / B, "decode_s_per_field": S * GRID ** 3 * pair_s,
+                               "s_per_field": per_field}
+        out["sample"] = (f"oracle on {threads} threads: {nstep} U-Net forwards at B={B} ({unet_step:.3f} s each) + "
+                         f"one decode of {nl} latents x {npts} coords ({pairs} pairs, {dec_s:.1f} s); extrapolated "
+                         f"to 256 steps per {B} samples + {S} x {GRID ** 3} pairs per field")
+    else:
+        per_field = C_COORDS * pair_s
+        out["measured"] = {"decode_pairs": pairs, "decode_s": dec_s, "ns_per_pair": pair_s * 1e9}
+        out["extrapolated"] = {"s_per_field": per_field}
+        out["sample"] = (f"oracle on {threads} threads: one decode of {nl} latents x {npts} coords ({pairs} pairs, "
+                         f"{dec_s:.1f} s); extrapolated to {C_COORDS} coords per field")
+    out["value"] = 1.0 / per_field
+    return out
+
+
+# ---------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", choices=["B", "C"], default="B")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--no-gather", action="store_true", help="keep decoded fields on their ranks")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--siren-compute", choices=["split_f16", "f32"], default="split_f16")
+    ap.add_argument("--unet-compute", choices=["split_f16", "fp32"], default="split_f16")
+    args = ap.parse_args()
+
+    rank, world, dev = init_dist()
+    from confild_amd import dist as cdist
+    gather = world > 1 and not args.no_gather
+
+    if args.config == "B":
+        o = setup_B(dev, rank, world, args.siren_compute, args.unet_compute)
+        nf = o["nf"]
+        shards = b_shards(args.scaling, world)
+        glob = sum(cnt for _, cnt in shards)
+        start, count = shards[rank]
+        sizes = [cnt * S for _, cnt in shards]
+
+        def one(k, ev=None):
+            f = step_B(o, dev, seed=10 ** 6 + k, start=start, count=count, ev=ev)
+            return gather_to_root(f, 0, sizes, world) if gather else f
+        c = CNF_B
+        npts = GRID ** 3
+        rows_local = count * S
+        fields_per_step = glob
+    else:
+        o = setup_C(dev, rank, world, args.siren_compute)
+        nf = o["nf"]
+        s, e = o["shard"]
+        sizes = [cdist.shard_range(C_COORDS, r, world)[1] - cdist.shard_range(C_COORDS, r, world)[0]
+                 for r in range(world)]
+
+        def one(k, ev=None):
+            if ev is not None:
+                ev[0].record()
+                ev[1].record()
+            f = nf.decode(o["coords"], o["lat"], o["xn"], o["yn"])                # (256, N_r, 3)
+            if ev is not None:
+                ev[2].record()
+            return gather_to_root(f, 1, sizes, world) if gather else f
+        c = CNF_C
+        npts = e - s
+        rows_local = C_LATENTS
+        fields_per_step = C_LATENTS
+    mode = nf.compute_mode(dev)
+    kname, peak, peak_basis, _ = ROOFLINE[mode]
+
+    for w in range(args.warmup):
+        one(-1 - w)
+    barrier(dev, world)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        out = one(k, evs[k])
+    barrier(dev, world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev, world)
+    unet_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in evs]))
+    dec_ms = float(np.mean([ev[1].elapsed_time(ev[2]) for ev in evs]))
+    value = fields_per_step * args.steps / elapsed
+    flops = rows_local * npts * siren_flops_per_pair(**c)
+    achieved = flops / (dec_ms / 1e3) / 1e12
+    if rank == 0 and out is not None:
+        assert torch.isfinite(out).all().item(), "non-finite output"
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline()
+            cpu = cpu_baseline(args.config)
+        par = (f"dp{world} ({'8 samples per GPU' if args.scaling == 'weak' else 'global batch 8 split'}"
+               f"{', fields gathered to rank 0' if gather else ''})") if args.config == "B" else \
+            f"coord-sharded over {world} GPU(s){', slabs gathered to rank 0' if gather else ''}"
+        if args.config == "B":
+            workload = (f"config B (Case4 uncond), {args.scaling} scaling: U-Net 64x64, global batch "
+                        f"{fields_per_step} ({count}/GPU), DDPM 256 steps (cosine, respaced), CNF SIREN(3,64,3,15,384) "
+                        f"decode of {S} latent rows per sample on the 64^3 lattice")
+        else:
+            workload = (f"config C (Case4 CNF-only): SIREN(3,384,3,15,384) decode of {C_LATENTS} latents x 2^22 "
+                        f"uniform coords, coordinate-sharded")
         rec = {
-            "metric": "generated fields/sec (256-step sample + CNF decode), Case4 latent, 1/2/4/8 GPU",
+            "metric": METRIC if args.config == "B" else
+            "decoded fields/sec (CNF-only, 2^22 coords per field), Case4 CNF, 1/2/4/8 GPU",
             "value": value, "unit": "fields/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": args.scaling if args.config == "B" else "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded weights and inputs; no checkpoints)",
             "compute": {"unet": ("fp32 via split-f16 convolutions (3x v_mfma_f32_16x16x32_f16 on 22-bit operand "
                                  "splits; error vs fp64 = fp32's, DESIGN.md K1s); GroupNorm/softmax/attention fp32"
-                                 if objs[0].compute == "split_f16" else "fp32 (v_mfma_f32_16x16x4_f32)"),
+                                 if args.config == "B" and o["model"].compute == "split_f16" else
+                                 "fp32 (v_mfma_f32_16x16x4_f32)" if args.config == "B" else None),
                         "cnf_decoder": ("fp32 via split-f16 (3x v_mfma_f32_32x32x16_f16 on 22-bit operand "
                                         "splits; error vs fp64 = fp32's, DESIGN.md K7t)" if mode == "split_f16"
                                         else "fp32 (v_mfma_f32_16x16x4_f32)")},
-            "config": {"workload": "Case4 uncond: U-Net 64x64 B=8/GPU, DDPM 256 steps (cosine, respaced), "
-                                   "CNF SIREN(3,64,3,15,384) decode of 8x64 latents on a 64^3 lattice",
-                       "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world} (independent batches)"},
+            "config": {"workload": workload, "global_batch": fields_per_step, "seq_len": S if args.config == "B"
+                       else C_COORDS, "parallelism": par},
             "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)", "achieved": achieved,
                          "peak": peak, "peak_basis": peak_basis, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": measured_traffic(mode, B * S, GRID ** 3), "flops_per_launch": flops,
-                         "launch_ms": dec_s * 1e3, "pmc": measured_mfma_util(kname),
-                         "unet_share_ms": (elapsed / args.steps - dec_s) * 1e3},
+                         "traffic": measured_traffic(mode, rows_local, npts) if args.config == "B" else None,
+                         "flops_per_launch": flops, "launch_ms": dec_ms, "pmc": measured_mfma_util(kname)},
             "cpu_baseline": cpu,
         }
+        if args.config == "B":
+            uf = count * UNET_FLOPS_PER_SAMPLE * 256
+            ua = uf / (unet_ms / 1e3) / 1e12
+            rec["roofline_unet"] = {"bound": "mfma", "kernel": "U-Net forward x 256 steps (all kernels + step)",
+                                    "achieved": ua, "peak": F16_PEAK_TFLOPS / 3,
+                                    "peak_basis": "f16 dense MFMA peak / 3 (split-f16 convolutions)",
+                                    "unit": "TFLOP/s", "frac": ua / (F16_PEAK_TFLOPS / 3), "flops": uf,
+                                    "ms": unet_ms, "ms_per_forward": unet_ms / 256}
         print(json.dumps(rec), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -104,8 +104,26 @@ def all_gather_cat(x: torch.Tensor, dim: int, sizes, group=None) -> torch.Tensor
 
 
 def gather_cat(x: torch.Tensor, dim: int, sizes, dst: int = 0, group=None):
-    """Like all_gather_cat but only `dst` receives (and returns) the result."""
+    """Like all_gather_cat but only `dst` receives (and returns) the result.
+    Along dim 0 the ranks' slabs land directly in their rows of the result (no
+    padding, no concatenation copy); other dims pad to the largest slab."""
     r, g = dist.get_rank(group), dist.get_world_size(group)
+    if dim == 0:
+        x = x.contiguous()
+        if r != dst:
+            if x.shape[0]:
+                dist.gather(x if x.shape[0] == max(sizes) else _pad0(x, max(sizes)), None, dst=dst, group=group)
+            else:
+                dist.gather(x.new_zeros((max(sizes),) + tuple(x.shape[1:])), None, dst=dst, group=group)
+            return None
+        mx = max(sizes)
+        if all(sz == mx for sz in sizes):
+            out = torch.empty((sum(sizes),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+            dist.gather(x, list(out.split(sizes)), dst=dst, group=group)
+            return out
+        outs = [torch.empty((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device) for _ in range(g)]
+        dist.gather(_pad0(x, mx), outs, dst=dst, group=group)
+        return torch.cat([o[:sizes[i]] for i, o in enumerate(outs)], 0)
     mx = max(sizes)
     pad = list(x.shape)
     pad[dim] = mx
@@ -116,6 +134,14 @@ def gather_cat(x: torch.Tensor, dim: int, sizes, dst: int = 0, group=None):
     if r != dst:
         return None
     return torch.cat([o.narrow(dim, 0, sizes[i]) for i, o in enumerate(outs)], dim=dim)
+
+
+def _pad0(x, n):
+    if x.shape[0] == n:
+        return x
+    buf = x.new_zeros((n,) + tuple(x.shape[1:]))
+    buf[:x.shape[0]].copy_(x)
+    return buf
 
 
 def sharded_decode(decode_fn, coords: torch.Tensor, latents: torch.Tensor, ymax=None, ymin=None, group=None):

@@ -146,3 +146,67 @@ def test_broadcast_bumps_parameter_version():
 
 def test_sharded_samples_rejects_batch_below_world():
     assert _run(_case_too_few_samples) == {0: "ValueError", 1: "ValueError"}
+
+
+def _case_gather_dim0(rank, world):
+    """gather_cat along dim 0: equal slabs land in place, uneven ones are padded."""
+    out = {}
+    for n in (2 * world, 2 * world + 1):
+        s, e = cdist.shard_range(n, rank, world)
+        x = torch.arange(s, e, dtype=torch.float32)[:, None].repeat(1, 3)
+        sizes = [cdist.shard_range(n, r, world)[1] - cdist.shard_range(n, r, world)[0] for r in range(world)]
+        g = cdist.gather_cat(x, 0, sizes, dst=0)
+        out[n] = None if g is None else g[:, 0].tolist()
+    return out
+
+
+def _case_bench_config_C(rank, world):
+    """bench.py config C's sharding: per-rank coordinate shards + per-point
+    normaliser rows, latents broadcast, slabs gathered to rank 0 along N --
+    equal to the unsharded decode (oracle compute, small sizes)."""
+    import bench
+    from oracle import siren as osn
+    d, L, c, nh, H = 3, 16, 3, 2, 32
+    sd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(3, d, L, c, nh, H).items()}
+    n_coords, n_lat = 1003, 4
+    coords, lat, ymax, ymin, (s, e) = bench.c_inputs(rank, world, n_coords, n_lat, L)
+    dist.broadcast(lat, src=0)
+    part = osn.decode(sd, coords, lat, torch.ones(1, 3), torch.zeros(1, 3), ymax, ymin)
+    sizes = [cdist.shard_range(n_coords, r, world)[1] - cdist.shard_range(n_coords, r, world)[0]
+             for r in range(world)]
+    full = bench.gather_to_root(part, 1, sizes, world)
+    if rank != 0:
+        return full is None
+    ac, al, ax, an, _ = bench.c_inputs(0, 1, n_coords, n_lat, L)
+    ref = osn.decode(sd, ac, al, torch.ones(1, 3), torch.zeros(1, 3), ax, an)
+    return bool(torch.equal(full, ref))
+
+
+def _case_bench_config_B(rank, world):
+    """bench.py config B's sample shards (weak and strong) gathered to rank 0 in
+    global sample order (stand-in compute: rows tagged by global sample index)."""
+    import bench
+    res = {}
+    for scaling in ("weak", "strong"):
+        shards = bench.b_shards(scaling, world)
+        start, count = shards[rank]
+        rows = torch.cat([torch.full((2, 3), float(start + i)) for i in range(count)])   # 2 rows per sample
+        g = bench.gather_to_root(rows, 0, [2 * cnt for _, cnt in shards], world)
+        res[scaling] = None if g is None else g[::2, 0].tolist()
+    return res
+
+
+def test_gather_cat_dim0_in_place_and_padded():
+    out = _run(_case_gather_dim0)
+    assert out[0] == {4: [0.0, 1.0, 2.0, 3.0], 5: [0.0, 1.0, 2.0, 3.0, 4.0]}, out
+    assert out[1] == {4: None, 5: None}
+
+
+def test_bench_config_C_sharding_equals_unsharded():
+    assert _run(_case_bench_config_C) == {0: True, 1: True}
+
+
+def test_bench_config_B_shards_weak_and_strong():
+    out = _run(_case_bench_config_B)
+    assert out[0] == {"weak": [float(i) for i in range(16)], "strong": [float(i) for i in range(8)]}, out
+    assert out[1] == {"weak": None, "strong": None}
