@@ -1,0 +1,610 @@
+// K1x: split-f16 implicit-GEMM convolution on v_mfma_f32_32x32x16_f16 with
+// 64x64 wave tiles and an in-workgroup K split (gfx950).
+//
+// Same GEMM view, operands and numerics as conv_gemm_kernel<..., MODE=2> (K1s,
+// unet_kernels.hip): M = B*Hout*Wout output pixels, N = Cout, K = ks*ks*Ctot
+// ordered (tap, channel); activations split x = xh + xl (f16 RNE) as they are
+// staged; weights pre-split (s w) = wh + wl; each product as wl.xh + wh.xl +
+// wh.xh with fp32 accumulation -- fp32-level error against fp64.
+//
+// What changes is the shape of the work, for the MFMA/LDS budget of a CU:
+//   * 32x32x16 MFMAs on 64x64 wave tiles: per 16-deep K sub-step a wave reads
+//     2+2 (hi, lo) A and B fragments (8 ds_read_b128) for 12 MFMAs of 32 cycles;
+//     K1s' 16x16x32 on 32x64 tiles reads 12 per 384 MFMA cycles -- 2x the LDS
+//     bytes per FLOP, and LDS, not the matrix pipe, bounded it;
+//   * KG wave groups split each workgroup's K range (group g takes K tiles
+//     g, g+KG, ...) and meet once through LDS at the end: KG x the waves per
+//     SIMD for latency hiding without split-K partial slabs in HBM.  The two
+//     partial sums are added in a fixed order (group 0 + group 1), so every
+//     output's summation order depends on the per-sample shape only (batch
+//     invariance, as split-K).
+// LDS rows are 32 f16 (64 B); the 16-B chunk c of row r sits in slot
+// c ^ ((r >> 2) & 3): every 16-lane group of a 32x32x16 fragment read
+// (ds_read_b128, lanes 0-31 rows 0-31 chunk 2s, lanes 32-63 chunk 2s+1) then
+// covers the 64 banks once; the 8-B staging writes stay conflict-free.
+#include <algorithm>
+
+#include "unet_kernels.hpp"
+
+namespace cfd {
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int xswz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+template <int BM, int BN, int WGM, int WGN, int KG>
+__global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs a) {
+    constexpr int NW = WGM * WGN * KG, NT = 64 * NW;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
+    constexpr int TM = WTM / 32, TN = WTN / 32;     // 32x32 blocks per wave
+    constexpr int RPP = NT / 8;                     // row-slices staged per pass (8 threads x 4 k)
+    constexpr int AIT = BM * KG / RPP, BIT = BN * KG / RPP;
+    static_assert(TM >= 1 && TN >= 1 && AIT >= 1 && BIT >= 1, "tile");
+    static_assert((BM * KG) % RPP == 0 && (BN * KG) % RPP == 0, "staging");
+    constexpr int ABYTES = BM * KG * 64, BBYTES = BN * KG * 64;    // one f16 plane
+    constexpr int STAGE = 2 * ABYTES + 2 * BBYTES;                 // A hi, A lo, B hi, B lo
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kg = wave / (WGM * WGN), wrem = wave % (WGM * WGN);
+    const int wm = wrem / WGN, wn = wrem % WGN;
+
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (a.xcd) {   // XCD-contiguous tile order, splits fastest (as conv_gemm_kernel)
+        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
+        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
+        bz = Lp % gz;
+        by = (Lp / gz) % gy;
+        bx = Lp / (gz * gy);
+    }
+    const int m0 = bx * BM, n0 = by * BN;
+    const int HWo = a.Hout * a.Wout;
+    const int kq = tid & 7, rsub = tid >> 3;
+
+    // staged row-slices: A (pixel m, group g), B (output channel n, group g)
+    int a_b[AIT], a_oy[AIT], a_ox[AIT], a_g[AIT], a_row[AIT];
+    bool a_ok[AIT];
+#pragma unroll
+    for (int it = 0; it < AIT; ++it) {
+        const int rs = rsub + it * RPP;
+        a_g[it] = rs / BM;
+        a_row[it] = rs;
+        const int m = m0 + rs % BM;
+        a_ok[it] = m < a.M;
+        const int mm = a_ok[it] ? m : 0;
+        a_b[it] = mm / HWo;
+        const int rem = mm - a_b[it] * HWo;
+        const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+        if (!a.up) {
+            a_oy[it] = oy * a.stride - a.pad;
+            a_ox[it] = ox * a.stride - a.pad;
+        } else {
+            a_oy[it] = oy - a.pad;
+            a_ox[it] = ox - a.pad;
+        }
+    }
+    const unsigned short* wrow_h[BIT];
+    const unsigned short* wrow_l[BIT];
+    int b_g[BIT], b_row[BIT];
+    bool b_ok[BIT];
+#pragma unroll
+    for (int it = 0; it < BIT; ++it) {
+        const int rs = rsub + it * RPP;
+        b_g[it] = rs / BN;
+        b_row[it] = rs;
+        const int n = n0 + rs % BN;
+        b_ok[it] = n < a.Cout;
+        wrow_h[it] = (const unsigned short*)a.wbf + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
+        wrow_l[it] = (const unsigned short*)a.wlo + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
+    }
+
+    const int nkt = a.K / 32;
+    const int per = (nkt + gridDim.z - 1) / gridDim.z;
+    const int kt0 = bz * per;
+    const int kt1 = min(nkt, kt0 + per);
+    // per-group K position (tap dy, dx and channel base) of tile kt0 + g, advanced by KG tiles
+    int cbg[KG], dyg[KG], dxg[KG];
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+        const int kb = (kt0 + g) * 32;
+        const int tap = kb / a.Ctot;
+        cbg[g] = kb - tap * a.Ctot;
+        dyg[g] = tap / a.ks;
+        dxg[g] = tap - dyg[g] * a.ks;
+    }
+
+    f4 ra[AIT];
+    uint2 rbh[BIT], rbl[BIT];
+    auto load_tile = [&](int kt) {   // tiles kt + g, g < KG
+#pragma unroll
+        for (int it = 0; it < AIT; ++it) {
+            const int g = a_g[it];
+            const int c0 = cbg[g] + 4 * kq, dy = dyg[g], dx = dxg[g];
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            int iy, ix;
+            bool ok = a_ok[it] && kt + g < kt1;
+            if (a.up) {
+                iy = a_oy[it] + dy;
+                ix = a_ox[it] + dx;
+                ok = ok && iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                iy >>= 1;
+                ix >>= 1;
+            } else {
+                iy = a_oy[it] + dy;
+                ix = a_ox[it] + dx;
+                ok = ok && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+            }
+            if (ok) {
+                const int64_t pix = ((int64_t)a_b[it] * a.Hin + iy) * a.Win + ix;
+                v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0)
+                              : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
+            }
+            ra[it] = v;
+        }
+#pragma unroll
+        for (int it = 0; it < BIT; ++it) {
+            const int g = b_g[it];
+            const bool ok = b_ok[it] && kt + g < kt1;
+            const int64_t koff = (int64_t)(kt + g) * 32;
+            rbh[it] = ok ? *(const uint2*)(wrow_h[it] + koff) : uint2{0u, 0u};
+            rbl[it] = ok ? *(const uint2*)(wrow_l[it] + koff) : uint2{0u, 0u};
+        }
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+            cbg[g] += 32 * KG;
+            while (cbg[g] >= a.Ctot) {
+                cbg[g] -= a.Ctot;
+                if (++dxg[g] == a.ks) {
+                    dxg[g] = 0;
+                    ++dyg[g];
+                }
+            }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* base = lds + buf * STAGE;
+#pragma unroll
+        for (int it = 0; it < AIT; ++it) {
+            const h4 hv = __builtin_convertvector(ra[it], h4);
+            const h4 lv = __builtin_convertvector(ra[it] - __builtin_convertvector(hv, f4), h4);
+            const int off = xswz(a_row[it], kq >> 1) + (kq & 1) * 8;
+            *(h4*)(base + off) = hv;
+            *(h4*)(base + ABYTES + off) = lv;
+        }
+#pragma unroll
+        for (int it = 0; it < BIT; ++it) {
+            const int off = xswz(b_row[it], kq >> 1) + (kq & 1) * 8;
+            *(uint2*)(base + 2 * ABYTES + off) = rbh[it];
+            *(uint2*)(base + 2 * ABYTES + BBYTES + off) = rbl[it];
+        }
+    };
+
+    f16v acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int l32 = lane & 31, hsel = lane >> 5;
+    const int arow0 = kg * BM + wm * WTM + l32, brow0 = kg * BN + wn * WTN + l32;
+    if (kt0 < kt1) {
+        load_tile(kt0);
+        store_tile(0);
+        __syncthreads();
+        int cur = 0;
+        for (int kt = kt0; kt < kt1; kt += KG) {
+            const bool more = kt + KG < kt1;
+            if (more) load_tile(kt + KG);
+            const char* base = lds + cur * STAGE;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int ch = 2 * s + hsel;
+                h8v fah[TM], fal[TM], fbh[TN], fbl[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int off = xswz(arow0 + 32 * i, ch);
+                    fah[i] = *(const h8v*)(base + off);
+                    fal[i] = *(const h8v*)(base + ABYTES + off);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int off = xswz(brow0 + 32 * j, ch);
+                    fbh[j] = *(const h8v*)(base + 2 * ABYTES + off);
+                    fbl[j] = *(const h8v*)(base + 2 * ABYTES + BBYTES + off);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                    }
+            }
+            if (more) store_tile(cur ^ 1);
+            __syncthreads();
+            cur ^= 1;
+        }
+    }
+
+    // combine the K groups through LDS: groups 1.. park their sums, group 0 adds
+    // them in group order (fixed summation order)
+    if constexpr (KG > 1) {
+        float* red = (float*)lds;   // (KG-1) x WGM*WGN waves x TM*TN*16 floats x 64 lanes
+        constexpr int PER_WAVE = TM * TN * 16 * 64;
+        static_assert((size_t)(KG - 1) * WGM * WGN * PER_WAVE * 4 <= 2 * STAGE, "reduction fits in the stages");
+        if (kg > 0) {
+            float* dst = red + ((kg - 1) * WGM * WGN + wrem) * PER_WAVE;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; e += 4)
+                        *(f4*)(dst + ((i * TN + j) * 16 + e) * 64 + 4 * lane) =
+                            f4{acc[i][j][e], acc[i][j][e + 1], acc[i][j][e + 2], acc[i][j][e + 3]};
+        }
+        __syncthreads();
+        if (kg > 0) return;
+#pragma unroll
+        for (int g = 1; g < KG; ++g) {
+            const float* src = red + ((g - 1) * WGM * WGN + wrem) * PER_WAVE;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; e += 4) {
+                        const f4 v = *(const f4*)(src + ((i * TN + j) * 16 + e) * 64 + 4 * lane);
+                        acc[i][j][e] += v[0];
+                        acc[i][j][e + 1] += v[1];
+                        acc[i][j][e + 2] += v[2];
+                        acc[i][j][e + 3] += v[3];
+                    }
+        }
+    }
+
+    // undo the power-of-two weight scale (exact); epilogue as conv_gemm_kernel
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] *= a.acc_scale;
+    const int n_base = n0 + wn * WTN + l32;
+    const int m_base = m0 + wm * WTM + 4 * hsel;
+    if (gridDim.z > 1) {
+        float* part = a.part + (int64_t)bz * a.M * a.Cout;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m_base + 32 * i + 8 * (e >> 2) + (e & 3);
+                if (m >= a.M) continue;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n_base + 32 * j;
+                    if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][e];
+                }
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int m = m_base + 32 * i + 8 * (e >> 2) + (e & 3);
+            if (m >= a.M) continue;
+            const int bb = m / HWo;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n_base + 32 * j;
+                if (n >= a.Cout) continue;
+                float v = a.bias ? acc[i][j][e] + a.bias[n] : acc[i][j][e];
+                if (a.emb) v = v + a.emb[(int64_t)bb * a.emb_stride + n];
+                if (a.res) v = a.res[(int64_t)m * a.Cout + n] + v;
+                a.out[(int64_t)m * a.Cout + n] = v;
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------
+// K1y: the same GEMM with every operand staged by LDS-DMA into an S-stage LDS
+// ring (buffer_load ... lds: no VGPR staging, S-1 K tiles in flight per
+// workgroup).  The activation tile lands as fp32 (im2col rows gathered per
+// lane, padding taps read as zeros by the buffer range check) and is split into
+// hi/lo f16 as each wave reads its fragments; weights land pre-split.
+// Workgroup 128x128 of 4 waves (one per SIMD), 64x64 wave tiles of 32x32x16
+// MFMAs.  LDS layouts (DMA lane order chosen so the fragment reads are
+// conflict-free): A rows 128 B, 16-B chunk c of row r in slot c ^ ((r>>1)&7);
+// B rows 64 B (xswz).
+__device__ __forceinline__ int yswzA(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
+constexpr int ywait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
+
+__device__ __forceinline__ void split8_mix(const f4& x0, const f4& x1, h8v& hi, h8v& lo) {
+    unsigned hw[4], lw[4];
+    const float xs[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const float a = xs[2 * w], b = xs[2 * w + 1];
+        hw[w] = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, h2));
+        unsigned l;
+        asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(l) : "v"(a), "v"(hw[w]));
+        asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hw[w]));
+        lw[w] = l;
+    }
+    hi = __builtin_bit_cast(h8v, (u4){hw[0], hw[1], hw[2], hw[3]});
+    lo = __builtin_bit_cast(h8v, (u4){lw[0], lw[1], lw[2], lw[3]});
+}
+
+// EXP (timing experiments only, wrong results): bit 0 no hi/lo split (A bits
+// reinterpreted), bit 1 no per-tap address arithmetic, bit 2 no A DMA at all
+// KORD: K tile order -- 0 (tap, channel chunk) as the weight packing, 1 (channel
+// chunk, tap): the 9 taps of one 32-channel chunk run back to back, so the
+// activation rows they re-read are still in L1/L2 (the summation order changes,
+// still a function of the per-sample shape only).
+template <int S, int EXP = 0, int KORD = 0>
+__global__ __launch_bounds__(256, 1) void conv_y_kernel(ConvArgs a) {
+    constexpr int BM = 128, BN = 128;
+    constexpr int ABYTES = BM * 32 * 4, BPLANE = BN * 32 * 2, STAGE = ABYTES + 2 * BPLANE;
+    constexpr int PPW = 8;   // DMA pieces per wave per K tile: 4 A + 2 B hi + 2 B lo
+    __shared__ __attribute__((aligned(1024))) char lds[S * STAGE];
+    __shared__ int pixtab[9 * BM];   // source pixel of (tap, tile row), -1: padding
+    typedef __attribute__((address_space(3))) void lds_t;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (a.xcd) {
+        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
+        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
+        bz = Lp % gz;
+        by = (Lp / gz) % gy;
+        bx = Lp / (gz * gy);
+    }
+    const int m0 = bx * BM, n0 = by * BN;
+    const int HWo = a.Hout * a.Wout;
+
+    // (tap, row) -> source pixel table, once per workgroup
+    const int ntap = a.ks * a.ks;
+    for (int e = threadIdx.x; e < ntap * BM; e += 256) {
+        const int tap = e / BM, r = e - tap * BM;
+        const int dy = tap / a.ks, dx = tap - dy * a.ks;
+        const int m = m0 + r;
+        int pix = -1;
+        if (m < a.M) {
+            const int b = m / HWo, rem = m - b * HWo;
+            const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+            int iy = (a.up ? oy - a.pad : oy * a.stride - a.pad) + dy;
+            int ix = (a.up ? ox - a.pad : ox * a.stride - a.pad) + dx;
+            bool ok;
+            if (a.up) {
+                ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                iy >>= 1;
+                ix >>= 1;
+            } else {
+                ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+            }
+            if (ok) pix = (b * a.Hin + iy) * a.Win + ix;
+        }
+        pixtab[e] = pix;
+    }
+    // A rows of this lane's 4 pieces (piece 4*wave + i covers rows 8 piece .. +7)
+    int a_r[4], a_c16[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a_r[i] = (4 * wave + i) * 8 + (lane >> 3);
+        a_c16[i] = 16 * ((lane & 7) ^ ((a_r[i] >> 1) & 7));
+    }
+    // B rows of this lane's 2 pieces per plane (piece 2*wave + j covers rows 16 piece .. +15)
+    unsigned b_off[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int r = (2 * wave + j) * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ ((r >> 2) & 3);
+        const int n = n0 + r;
+        b_off[j] = n < a.Cout ? (unsigned)(((int64_t)n * a.K + 8 * c) * 2) : 0x80000000u;
+    }
+    const int srows = a.Hin * a.Win * (a.M / HWo);   // input pixels of the whole batch
+    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
+
+    const int nkt = a.K / 32;
+    const int per = (nkt + gridDim.z - 1) / gridDim.z;
+    const int kt0 = bz * per;
+    const int kt1 = min(nkt, kt0 + per);
+
+    // K position of the next tile to issue: tap, channel base (advanced per issue)
+    int itap, icb;
+    if (KORD == 0) {
+        itap = (kt0 * 32) / a.Ctot;
+        icb = kt0 * 32 - itap * a.Ctot;
+    } else {
+        icb = 32 * (kt0 / ntap);
+        itap = kt0 - (icb / 32) * ntap;
+    }
+    auto issue = [&](int t, int stage) {
+        const int tap = itap, cb = icb;
+        if (KORD == 0) {
+            icb += 32;
+            if (icb == a.Ctot) {
+                icb = 0;
+                ++itap;
+            }
+        } else if (++itap == ntap) {
+            itap = 0;
+            icb += 32;
+        }
+        const bool second = cb >= a.C1;
+        const unsigned csrc4 = 4u * (second ? a.C2 : a.C1), cofs4 = 4u * (second ? cb - a.C1 : cb);
+        const int kb = t * 32;
+        char* sb = lds + stage * STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if constexpr ((EXP & 4) != 0) continue;
+            if constexpr ((EXP & 2) != 0) {
+                lds_t* dst = (lds_t*)(sb + (4 * wave + i) * 1024);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, dst, 16, a_c16[i] + lane * 64, kb * 4, 0, 0);
+                continue;
+            }
+            const int pix = pixtab[tap * BM + a_r[i]];
+            const unsigned off = pix >= 0 ? __umul24((unsigned)pix, csrc4) + (cofs4 + a_c16[i])
+                                          : 0x80000000u;
+            lds_t* dst = (lds_t*)(sb + (4 * wave + i) * 1024);
+            if (second)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs2, dst, 16, off, 0, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, dst, 16, off, 0, 0, 0);
+        }
+        const int kofs = (tap * a.Ctot + cb) * 2;   // bytes of this K tile in a (tap, channel) weight row
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const unsigned off = b_off[j] == 0x80000000u ? b_off[j] : b_off[j] + kofs;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rwh, (lds_t*)(sb + ABYTES + (2 * wave + j) * 1024), 16, off, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rwl, (lds_t*)(sb + ABYTES + BPLANE + (2 * wave + j) * 1024), 16,
+                                                     off, 0, 0, 0);
+        }
+    };
+
+    f16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    const int l32 = lane & 31, hsel = lane >> 5;
+    const int arow = wm * 64 + l32, brow = wn * 64 + l32;
+
+    __syncthreads();   // pixtab
+    for (int t = 0; t < S - 1; ++t)
+        if (kt0 + t < kt1) issue(kt0 + t, t);
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const int ahead = min(S - 2, kt1 - 1 - kt);   // tiles issued after kt
+        if (ahead >= 2) __builtin_amdgcn_s_waitcnt(ywait(2 * PPW));
+        else if (ahead == 1) __builtin_amdgcn_s_waitcnt(ywait(PPW));
+        else __builtin_amdgcn_s_waitcnt(ywait(0));
+        __syncthreads();
+        if (kt + S - 1 < kt1) issue(kt + S - 1, (kt - kt0 + S - 1) % S);
+        const char* sb = lds + ((kt - kt0) % S) * STAGE;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            h8v fah[2], fal[2], fbh[2], fbl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = arow + 32 * i;
+                if constexpr ((EXP & 1) != 0) {
+                    fah[i] = *(const h8v*)(sb + yswzA(row, 4 * s + 2 * hsel));
+                    fal[i] = *(const h8v*)(sb + yswzA(row, 4 * s + 2 * hsel + 1));
+                } else {
+                    const f4 x0 = *(const f4*)(sb + yswzA(row, 4 * s + 2 * hsel));
+                    const f4 x1 = *(const f4*)(sb + yswzA(row, 4 * s + 2 * hsel + 1));
+                    split8_mix(x0, x1, fah[i], fal[i]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int off = xswz(brow + 32 * j, 2 * s + hsel);
+                fbh[j] = *(const h8v*)(sb + ABYTES + off);
+                fbl[j] = *(const h8v*)(sb + ABYTES + BPLANE + off);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+    }
+
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] *= a.acc_scale;
+    const int n_base = n0 + wn * 64 + l32;
+    const int m_base = m0 + wm * 64 + 4 * hsel;
+    if (gridDim.z > 1) {
+        float* part = a.part + (int64_t)bz * a.M * a.Cout;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m_base + 32 * i + 8 * (e >> 2) + (e & 3);
+                if (m >= a.M) continue;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int n = n_base + 32 * j;
+                    if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][e];
+                }
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int m = m_base + 32 * i + 8 * (e >> 2) + (e & 3);
+            if (m >= a.M) continue;
+            const int bb = m / HWo;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = n_base + 32 * j;
+                if (n >= a.Cout) continue;
+                float v = a.bias ? acc[i][j][e] + a.bias[n] : acc[i][j][e];
+                if (a.emb) v = v + a.emb[(int64_t)bb * a.emb_stride + n];
+                if (a.res) v = a.res[(int64_t)m * a.Cout + n] + v;
+                a.out[(int64_t)m * a.Cout + n] = v;
+            }
+        }
+}
+
+// variant ids (tools/convbench): BM x BN, wave grid, K groups
+int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
+    CFD_REQUIRE(a.wbf && a.wlo && !a.tmode, CFD_ESTATE, "conv_x: split-f16 forward only");
+    CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_x needs channels % 32 == 0");
+    CFD_REQUIRE(splits == 1 || a.part, CFD_ESTATE, "split-K needs a partial buffer");
+    if (variant >= 10) {   // K1y: 32-bit buffer offsets
+        const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
+        CFD_REQUIRE(srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * 2 < (1ll << 31),
+                    CFD_ESHAPE, "conv_y: operands beyond 2 GiB");
+    }
+    auto grid = [&](int bm, int bn) {
+        return dim3((unsigned)ceil_div(a.M, bm), (unsigned)ceil_div(a.Cout, bn), splits);
+    };
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 2>), grid(128, 128), dim3(512), 0, st, a); break;
+        case 1: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1>), grid(256, 128), dim3(512), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((conv_x_kernel<128, 64, 2, 1, 2>), grid(128, 64), dim3(256), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((conv_x_kernel<64, 128, 1, 2, 2>), grid(64, 128), dim3(256), 0, st, a); break;
+        case 10: hipLaunchKernelGGL((conv_y_kernel<4>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 11: hipLaunchKernelGGL((conv_y_kernel<3>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 12: hipLaunchKernelGGL((conv_y_kernel<4, 1>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 13: hipLaunchKernelGGL((conv_y_kernel<4, 3>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 14: hipLaunchKernelGGL((conv_y_kernel<4, 5>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 15: hipLaunchKernelGGL((conv_y_kernel<4, 0, 1>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 16: hipLaunchKernelGGL((conv_y_kernel<4, 1, 1>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 17: hipLaunchKernelGGL((conv_y_kernel<3, 0, 1>), grid(128, 128), dim3(256), 0, st, a); break;
+        default: CFD_REQUIRE(false, CFD_EARG, "conv_x variant");
+    }
+    check_launch("conv_x_kernel");
+    return splits;
+}
+
+}  // namespace cfd

@@ -397,6 +397,19 @@ __device__ __forceinline__ int lds_swz_bf(int row, int chunk) {
     return row * 64 + ((chunk + 2 * ((row >> 2) & 1)) & 3) * 16;
 }
 
+// hi = f16(x) (RNE), lo = f16(x - hi) for 4 values: two packed converts and four
+// v_fma_mix (x - hi is exact in fp32, so lo carries one rounding, as before)
+__device__ __forceinline__ void split4_mix(const f4& x, uint2& hi, uint2& lo) {
+    typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+    typedef float f2_ __attribute__((ext_vector_type(2)));
+    hi.x = __builtin_bit_cast(unsigned, __builtin_convertvector((f2_){x[0], x[1]}, h2_));
+    hi.y = __builtin_bit_cast(unsigned, __builtin_convertvector((f2_){x[2], x[3]}, h2_));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.x) : "v"(x[0]), "v"(hi.x));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.x) : "v"(x[1]), "v"(hi.x));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.y) : "v"(x[2]), "v"(hi.y));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.y) : "v"(x[3]), "v"(hi.y));
+}
+
 // SPLIT (MODE 2, default fp32 path): fp32-accurate convolution on f16 MFMA.
 // Activations are split as staged, x = xh + xl (xh = f16(x), xl = f16(x - xh),
 // RNE); weights come pre-split from the host as (s w) = wh + wl with a
@@ -407,7 +420,7 @@ __device__ __forceinline__ int lds_swz_bf(int row, int chunk) {
 // (tests/test_gpu_unet_split.py).  hi and lo tiles use the bf16 LDS layout.
 // NW waves as (NW/2) x 2; 8 waves with BM = 128 halve the weight-tile reads per
 // output pixel at the same per-wave tile.
-template <int BM, int BN, bool TMODE, int MODE, int NW = 4>
+template <int BM, int BN, bool TMODE, int MODE, int NW = 4, bool BUFA = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(ConvArgs a) {
     constexpr bool BF = MODE == 1, SP = MODE == 2;
     constexpr int BK = 32;
@@ -420,6 +433,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     constexpr int AFL = BF ? BM * BK / 2 : BM * BK, BFL = BF ? BN * BK / 2 : BN * BK;
     __shared__ __attribute__((aligned(16))) float As[2][AFL];
     __shared__ __attribute__((aligned(16))) float Bs[2][BFL];
+    // buffer-addressed forward (a.bufaddr): source pixel of every (tap, tile row),
+    // -1 for padding, built once per workgroup; the tile loads then cost one table
+    // read, one 24-bit multiply-add and a select per row instead of the 64-bit
+    // index arithmetic that made the kernel VALU-issue-bound
+    __shared__ int pixtab[BUFA ? 9 * BM : 1];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -482,11 +500,20 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     const int kt0 = bz * per;
     const int kt1 = min(nkt, kt0 + per);
     // wave-uniform K position: (dy, dx) tap and channel base, advanced per tile
+    // in (tap, chunk) order or, with a.korder, (chunk, tap) order: the taps of one
+    // 32-channel chunk back to back re-read activation rows while they are in L2
     int cb = 0, dy = 0, dx = 0;
     {
-        const int kb = kt0 * BK;
-        const int tap = kb / a.Ctot;
-        cb = kb - tap * a.Ctot;
+        const int ntap = a.ks * a.ks;
+        int tap;
+        if (a.korder) {
+            cb = BK * (kt0 / ntap);
+            tap = kt0 - (kt0 / ntap) * ntap;
+        } else {
+            const int kb = kt0 * BK;
+            tap = kb / a.Ctot;
+            cb = kb - tap * a.Ctot;
+        }
         dy = tap / a.ks;
         dx = tap - dy * a.ks;
     }
@@ -494,8 +521,74 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     const int smask = a.stride - 1, sshift = a.stride >> 1;
     f4 ra[AIT], rb[BIT];
     uint2 rbh[BIT], rbl[BIT];
+    // buffer-addressed path: resources, per-row weight offsets, the pixel table
+    constexpr int WES = (BF || SP) ? 2 : 4;   // weight element bytes
+    const int srows = a.Hin * a.Win * (a.M / HWo);
+    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((BF || SP) ? (const void*)a.wbf : (const void*)a.w), 0, a.Cout * a.K * WES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(SP ? (const void*)a.wlo : (const void*)a.w), 0, a.Cout * a.K * WES, 0x00020000);
+    unsigned b_voff[BIT];
+    if constexpr (BUFA) {
+#pragma unroll
+        for (int it = 0; it < BIT; ++it) {
+            const int n = n0 + rsub + it * RPP;
+            b_voff[it] = n < a.Cout ? (unsigned)((n * a.K + 4 * kq) * WES) : 0x80000000u;
+        }
+        const int ntap = a.ks * a.ks;
+        for (int e = tid; e < ntap * BM; e += 64 * NW) {
+            const int tap = e / BM, r = e - tap * BM;
+            const int ty = tap / a.ks, tx = tap - ty * a.ks;
+            const int m = m0 + r;
+            int pix = -1;
+            if (m < a.M) {
+                const int b = m / HWo, rem = m - b * HWo;
+                const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+                int iy = (a.up ? oy - a.pad : oy * a.stride - a.pad) + ty;
+                int ix = (a.up ? ox - a.pad : ox * a.stride - a.pad) + tx;
+                bool ok;
+                if (a.up) {
+                    ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                    iy >>= 1;
+                    ix >>= 1;
+                } else {
+                    ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+                }
+                if (ok) pix = (b * a.Hin + iy) * a.Win + ix;
+            }
+            pixtab[e] = pix;
+        }
+        __syncthreads();
+    }
     auto load_tile = [&](int kt) {
         const int c0 = cb + 4 * kq;
+        const int kpos = (dy * a.ks + dx) * a.Ctot + cb;   // this tile's offset in a (tap, channel) weight row
+        if constexpr (BUFA) {
+            const int tap = dy * a.ks + dx;
+            const bool second = cb >= a.C1;
+            const unsigned csrc4 = 4u * (second ? a.C2 : a.C1);
+            const unsigned cofs4 = 4u * (second ? c0 - a.C1 : c0);
+            const __amdgpu_buffer_rsrc_t rsa = second ? rs2 : rs1;
+#pragma unroll
+            for (int it = 0; it < AIT; ++it) {
+                const int pix = pixtab[tap * BM + rsub + it * RPP];
+                const unsigned off = pix >= 0 ? __umul24((unsigned)pix, csrc4) + cofs4 : 0x80000000u;
+                ra[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
+            }
+            const int soff = kpos * WES;
+#pragma unroll
+            for (int it = 0; it < BIT; ++it) {
+                if constexpr (BF || SP)
+                    rbh[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, b_voff[it], soff, 0));
+                if constexpr (SP)
+                    rbl[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, b_voff[it], soff, 0));
+                if constexpr (!BF && !SP)
+                    rb[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rwh, b_voff[it], soff, 0));
+            }
+        } else {
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             f4 v = {0.f, 0.f, 0.f, 0.f};
@@ -529,18 +622,29 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
             if constexpr (BF || SP)
-                rbh[it] = b_ok[it] ? *(const uint2*)(wrow_bf[it] + kt * BK) : uint2{0u, 0u};
+                rbh[it] = b_ok[it] ? *(const uint2*)(wrow_bf[it] + kpos) : uint2{0u, 0u};
             if constexpr (SP)
-                rbl[it] = b_ok[it] ? *(const uint2*)(wrow_lo[it] + kt * BK) : uint2{0u, 0u};
+                rbl[it] = b_ok[it] ? *(const uint2*)(wrow_lo[it] + kpos) : uint2{0u, 0u};
             if constexpr (!BF && !SP)
-                rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kt * BK) : f4{0.f, 0.f, 0.f, 0.f};
+                rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kpos) : f4{0.f, 0.f, 0.f, 0.f};
         }
-        cb += BK;
-        if (cb >= a.Ctot) {
-            cb = 0;
+        }
+        if (a.korder) {
             if (++dx == a.ks) {
                 dx = 0;
-                ++dy;
+                if (++dy == a.ks) {
+                    dy = 0;
+                    cb += BK;
+                }
+            }
+        } else {
+            cb += BK;
+            if (cb >= a.Ctot) {
+                cb = 0;
+                if (++dx == a.ks) {
+                    dx = 0;
+                    ++dy;
+                }
             }
         }
     };
@@ -549,11 +653,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             // hi tile at [0, BM*BK/2) floats, lo tile after it (same bf16 layout)
 #pragma unroll
             for (int it = 0; it < AIT; ++it) {
-                const h4 hv = __builtin_convertvector(ra[it], h4);
-                const h4 lv = __builtin_convertvector(ra[it] - __builtin_convertvector(hv, f4), h4);
+                // hi = f16(x) (RNE, packed convert), lo = f16(x - hi) in one v_fma_mix per value
+                uint2 hv, lv;
+                split4_mix(ra[it], hv, lv);
                 const int off = lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8;
-                *(h4*)((char*)As[buf] + off) = hv;
-                *(h4*)((char*)As[buf] + BM * BK * 2 + off) = lv;
+                *(uint2*)((char*)As[buf] + off) = hv;
+                *(uint2*)((char*)As[buf] + BM * BK * 2 + off) = lv;
             }
 #pragma unroll
             for (int it = 0; it < BIT; ++it) {
@@ -1232,18 +1337,26 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     return p;
 }
 
+template <bool TMODE, int MODE, bool BUFA>
+static void launch_conv_tiles_(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
+    if (p.nw == 8 && p.bm == 128 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE, 8, BUFA>), grid, dim3(512), 0, st, a);
+    else if (p.bm == 128 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE, 4, BUFA>), grid, dim3(256), 0, st, a);
+    else if (p.bm == 64 && p.bn == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE, MODE, 4, BUFA>), grid, dim3(256), 0, st, a);
+    else if (p.bm == 128 && p.bn == 64)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, 64, TMODE, MODE, 4, BUFA>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE, MODE, 4, BUFA>), grid, dim3(256), 0, st, a);
+}
+
 template <bool TMODE, int MODE>
 static void launch_conv_tiles(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-    if (p.nw == 8 && p.bm == 128 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE, 8>), grid, dim3(512), 0, st, a);
-    else if (p.bm == 128 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE>), grid, dim3(256), 0, st, a);
-    else if (p.bm == 64 && p.bn == 128)
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 128, TMODE, MODE>), grid, dim3(256), 0, st, a);
-    else if (p.bm == 128 && p.bn == 64)
-        hipLaunchKernelGGL((conv_gemm_kernel<128, 64, TMODE, MODE>), grid, dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL((conv_gemm_kernel<64, 64, TMODE, MODE>), grid, dim3(256), 0, st, a);
+    if constexpr (!TMODE) {
+        if (a.bufaddr) return launch_conv_tiles_<false, MODE, true>(a, p, grid, st);
+    }
+    launch_conv_tiles_<TMODE, MODE, false>(a, p, grid, st);
 }
 
 void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st) {
@@ -1260,8 +1373,17 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
     CFD_REQUIRE(!(a.tmode && a.wbf && !a.wlo), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
     static const int xcd = env_int("CFD_CONV_XCD", 1);
+    static const int korder = env_int("CFD_CONV_KORDER", 0);
+    static const int bufaddr = env_int("CFD_CONV_BUFADDR", 1);
     ConvArgs b = a;
     b.xcd = xcd ? 1 : 0;
+    b.korder = korder ? 1 : 0;
+    {   // 32-bit buffer offsets and 24-bit pixel indices must hold
+        const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
+        const int64_t wes = (a.wbf || a.wlo) ? 2 : 4;
+        b.bufaddr = bufaddr && !a.tmode && a.ks * a.ks <= 9 && srows < (1 << 24) &&
+                    srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * wes < (1ll << 31);
+    }
     const ConvArgs& a_ = b;
     if (a.tmode && a.wlo)
         launch_conv_tiles<true, 2>(a_, p, grid, st);

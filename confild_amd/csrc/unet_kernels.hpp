@@ -51,6 +51,8 @@ struct ConvArgs {
     int emb_stride;
     int M, K;
     int xcd;             // XCD-contiguous workgroup order (set by launch_conv; CFD_CONV_XCD=0: off)
+    int korder;          // K tile order: 0 (tap, channel chunk), 1 (channel chunk, tap) (set by launch_conv)
+    int bufaddr;         // 32-bit buffer addressing of the operands (set by launch_conv where it fits)
 };
 
 struct AttnArgs {
@@ -110,6 +112,9 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats);
 // launched: the caller runs launch_splitk_reduce or hands the slab to launch_gn.
 int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer = false);
 void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st);
+// K1x (conv_x.hip): split-f16 forward convolution on 32x32x16 MFMAs with 64x64
+// wave tiles and an in-workgroup K split; variant selects the tile shape
+int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st);
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
 void launch_conv_out(const ConvArgs& a, hipStream_t st);
 void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t st);
