@@ -250,6 +250,63 @@ def b_shards(scaling, world):
 
 
 # ---------------------------------------------------------------------------
+# config D (guided DPS loop at the config-B widths) and the real Case4 notebook
+# shapes (384^2 latent, channel_mult 1,1,2,2,4,4, SIREN(3,384,3,15,384), 1000 steps)
+# ---------------------------------------------------------------------------
+DPS_CFG = {
+    "D": dict(size=64, channel_mult="", siren=(3, 64, 3, 15, 384), respacing="256", batch=8),
+    "Case4": dict(size=384, channel_mult="1, 1, 2, 2, 4, 4", siren=(3, 384, 3, 15, 384), respacing="",
+                  batch=1),
+}
+
+
+def setup_dps(dev, rank, world, which, batch):
+    """The notebook's objects (inference_phy_random_sensor.ipynb cells 11-20) with
+    synthetic weights: guided create_model, a Case4 operator with 10 sensors, 'ps'
+    conditioning (scale 1, sigma 0), the 'ddpm' sampler."""
+    import functools
+    from confild_amd import dist as cdist
+    from confild_amd import synth
+    from confild_amd.guided.condition_methods import get_conditioning_method
+    from confild_amd.guided.gaussian_diffusion import create_sampler
+    from confild_amd.guided.measurements import Case4Operator, get_noise
+    from confild_amd.guided.unet import create_model as guided_model
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    from confild_amd.normalize import Normalizer_ts
+    c = DPS_CFG[which]
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")   # no model_path: weights are set (or broadcast) below
+        m = guided_model(image_size=c["size"], num_channels=128, num_res_blocks=2, channel_mult=c["channel_mult"],
+                         num_heads=4, num_head_channels=64, attention_resolutions="32,16,8")
+    d, L, co, nh, H = c["siren"]
+    nf = SIRENAutodecoder_film(d, L, co, nh, H)
+    if rank == 0:
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in
+                           synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()}).items()})
+        nf.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, d, L, co, nh, H).items()})
+    m.to(dev)
+    nf.to(dev)
+    cdist.broadcast_module(m)
+    cdist.broadcast_module(nf)
+    ns = 10
+    coords = torch.from_numpy(synth.uniform(5, "dps/sensors", (ns, d), 0.0, 1.0))
+    xn = Normalizer_ts(params=(torch.ones(1, d), torch.zeros(1, d)), method="-11", dim=0)
+    yn = Normalizer_ts(params=(torch.full((co,), 2.0), torch.full((co,), -2.0)), method="-11", dim=0)
+    op = Case4Operator.from_parts(dev, coords, xn, yn, nf, torch.full((L,), 1.5), torch.full((L,), -1.5),
+                                  batch_size=384)
+    cond = get_conditioning_method(operator=op, noiser=get_noise(sigma=0.0, name="gaussian"), name="ps", scale=1.0)
+    smp = create_sampler(sampler="ddpm", steps=1000, noise_schedule="cosine", model_mean_type="epsilon",
+                         model_var_type="fixed_large", dynamic_threshold=False, clip_denoised=True,
+                         rescale_timesteps=False, timestep_respacing=c["respacing"])
+    # the measurement: the operator applied to a fixed latent
+    S = c["size"]
+    x_true = torch.from_numpy(synth.uniform(6, "dps/xtrue", (1, 1, S, L), -0.9, 0.9)).to(dev)
+    y = op.forward(x_true)
+    return dict(model=m, op=op, cond=cond, sampler=smp, fn=functools.partial(cond.conditioning), y=y, S=S, L=L)
+
+
+# ---------------------------------------------------------------------------
 # CPU baseline (oracle on this host's cores)
 # ---------------------------------------------------------------------------
 def _cpu_info():
@@ -357,7 +414,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=["B", "C"], default="B")
+    ap.add_argument("--config", choices=["B", "C", "D", "Case4"], default="B")
+    ap.add_argument("--dps-steps", type=int, default=0,
+                    help="D / Case4: time this many reverse steps of the loop (0: the whole loop)")
+    ap.add_argument("--batch", type=int, default=0, help="D / Case4: chains per GPU (0: the config's)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-gather", action="store_true", help="keep decoded fields on their ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -369,6 +429,8 @@ def main():
     from confild_amd import dist as cdist
     gather = world > 1 and not args.no_gather
 
+    if args.config in ("D", "Case4"):
+        return main_dps(args, rank, world, dev)
     if args.config == "B":
         o = setup_B(dev, rank, world, args.siren_compute, args.unet_compute)
         nf = o["nf"]
@@ -466,6 +528,62 @@ def main():
                                     "peak_basis": "f16 dense MFMA peak / 3 (split-f16 convolutions)",
                                     "unit": "TFLOP/s", "frac": ua / (F16_PEAK_TFLOPS / 3), "flops": uf,
                                     "ms": unet_ms, "ms_per_forward": unet_ms / 256}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def main_dps(args, rank, world, dev):
+    """Guided DPS loop (C/gaussian_diffusion.py:169-206 with 'ps' conditioning):
+    config D = the 256-step loop at config-B widths, B chains per GPU; Case4 = the
+    notebook's 384^2 1000-step loop (its published 9.26-9.35 it/s at one sample,
+    inference_phy_random_sensor.ipynb:321-330).  A step = one chain-batch reverse
+    step (U-Net forward with tape, DDPM step, SIREN at the sensors, latent
+    gradient, U-Net input-VJP, update); it/s = steps x chains / s.  With
+    --dps-steps the loop is timed over its first K steps (every step costs the
+    same)."""
+    from confild_amd import synth
+    c = DPS_CFG[args.config]
+    batch = args.batch or c["batch"]
+    o = setup_dps(dev, rank, world, args.config, batch)
+    smp = o["sampler"]
+    nsteps = smp.num_timesteps
+    timed = min(args.dps_steps, nsteps) if args.dps_steps else nsteps
+    x0 = torch.from_numpy(synth.normal(1000 + rank, "dps/xT", (batch, 1, o["S"], o["L"]))).to(dev)
+
+    def run(k_steps, seed):
+        x = x0.clone()
+        dist_buf = torch.zeros(batch, device=dev)
+        for k, i in enumerate(range(nsteps - 1, nsteps - 1 - k_steps, -1)):
+            x = smp._guided_step(o["model"], x, i, o["y"], o["cond"], None, seed, k, rank * batch, dist_buf)[0]
+        return x
+
+    for w in range(args.warmup):
+        run(min(3, timed), 7 + w)
+    barrier(dev, world)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        out = run(timed, 100 + k)
+    barrier(dev, world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev, world)
+    assert torch.isfinite(out).all().item(), "non-finite output"
+    o["model"].check_finite(dev)
+    steps_total = timed * args.steps
+    its = steps_total * batch * world / elapsed
+    if rank == 0:
+        rec = {"metric": "guided DPS reverse steps/sec (it/s summed over chains), Case4 conditional",
+               "value": its, "unit": "it/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": elapsed / steps_total * 1e3, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded weights and inputs; no checkpoints)",
+               "config": {"workload": (f"config {args.config}: guided 'ps' DDPM loop, U-Net {o['S']}^2 "
+                                       f"(channel_mult {c['channel_mult'] or 'default'}), SIREN{c['siren']} at 10 "
+                                       f"sensors, {nsteps}-step schedule, {timed} steps timed, {batch} chain(s)/GPU"),
+                          "global_batch": batch * world, "seq_len": o["S"],
+                          "parallelism": f"dp{world} (independent chains)"},
+               "reference_published": ("9.26-9.35 it/s at one chain, unstated NVIDIA GPU "
+                                       "(inference_phy_random_sensor.ipynb:321-330)") if args.config == "Case4" else None,
+               "per_chain_it_s": its / (batch * world)}
         print(json.dumps(rec), flush=True)
     if world > 1:
         import torch.distributed as dist

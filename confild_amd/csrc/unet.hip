@@ -72,6 +72,7 @@ struct cfd_unet {
     uint16_t* arena_thi = nullptr;  // split compute: f16 hi / lo parts of the scaled input-gradient packs
     uint16_t* arena_tlo = nullptr;
     int compute = CFD_COMPUTE_SPLIT_F16;
+    int* nonfinite = nullptr;  // range guard flag: set by the last convolution on a non-finite eps
 };
 
 namespace {
@@ -626,6 +627,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 a.Cout = c.out_channels;
                 a.M = B * cur.H * cur.W;
                 a.K = 9 * cur.Ca;
+                a.nonfinite = h->nonfinite;
                 flush();
                 if (launch) cfd::launch_conv_out(a, st);
                 break;
@@ -852,6 +854,8 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             const float nl = (float)(-std::log(10000.0));
             for (int i = 0; i < half; ++i) fr[i] = std::exp((nl * (float)i) / (float)half);
             CFD_HIP(hipMalloc(&h->freqs, sizeof(float) * std::max(half, 1)));
+            CFD_HIP(hipMalloc(&h->nonfinite, sizeof(int)));
+            CFD_HIP(hipMemset(h->nonfinite, 0, sizeof(int)));
             CFD_HIP(hipMemcpy(h->freqs, fr.data(), sizeof(float) * half, hipMemcpyHostToDevice));
         } catch (...) {
             cfd_unet_destroy(h);
@@ -873,6 +877,7 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->arena_lo);
     (void)hipFree(h->arena_thi);
     (void)hipFree(h->arena_tlo);
+    (void)hipFree(h->nonfinite);
     delete h;
 }
 
@@ -1107,5 +1112,18 @@ extern "C" int cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, i
         run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
         Workspace ws{align256(workspace), 0, false};
         run_vjp(h, d_eps, d_x, B, recs, ws, (hipStream_t)stream);
+    });
+}
+
+extern "C" int cfd_unet_check_finite(cfd_unet* h, int* nonfinite, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && nonfinite, CFD_EARG, "null argument");
+        cfd::DeviceGuard dg(h->device);
+        const hipStream_t st = (hipStream_t)stream;
+        int v = 0;
+        CFD_HIP(hipMemcpyAsync(&v, h->nonfinite, sizeof(int), hipMemcpyDeviceToHost, st));
+        CFD_HIP(hipMemsetAsync(h->nonfinite, 0, sizeof(int), st));
+        CFD_HIP(hipStreamSynchronize(st));
+        *nonfinite = v;
     });
 }

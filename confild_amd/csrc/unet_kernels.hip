@@ -863,7 +863,11 @@ __global__ void conv_out_kernel(ConvArgs a) {
     for (int n = 0; n < a.Cout; ++n) {
         float v = s[n];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0) a.out[m * a.Cout + n] = a.bias ? v + a.bias[n] : v;
+        if (lane == 0) {
+            const float y = a.bias ? v + a.bias[n] : v;
+            a.out[m * a.Cout + n] = y;
+            if (a.nonfinite && !isfinite(y)) *a.nonfinite = 1;
+        }
     }
 }
 
@@ -901,7 +905,13 @@ __global__ __launch_bounds__(256) void conv_out_vec_kernel(ConvArgs a, int LP) {
         if (n >= a.Cout) break;
         float v = s[n];
         for (int o = LP >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane % LP == 0 && m < a.M) a.out[m * a.Cout + n] = a.bias ? v + a.bias[n] : v;
+        if (lane % LP == 0 && m < a.M) {
+            const float y = a.bias ? v + a.bias[n] : v;
+            a.out[m * a.Cout + n] = y;
+            // range guard: an activation beyond the f16 range makes a split-f16 hi
+            // part infinite, and every such value reaches eps as inf / NaN
+            if (a.nonfinite && !isfinite(y)) *a.nonfinite = 1;
+        }
     }
 }
 

@@ -72,6 +72,14 @@ SRA, SRM1, M1, M2, SIGMA, SQRT_ABP, DIR, SIGMA_DDIM = range(8)
 STEP_DDPM, STEP_DDIM = 0, 1
 
 
+def check_model_range(model, device):
+    """The split-f16 range guard of a HIP U-Net (UNetModel.check_finite), if the
+    model has one; any other callable passes."""
+    fn = getattr(model, "check_finite", None)
+    if callable(fn):
+        fn(device)
+
+
 def fresh_seed(noise, seed):
     """The Philox key of a single step: the caller's, or (no explicit noise and no
     seed) a fresh draw from torch's default generator, so independent calls never
@@ -256,6 +264,8 @@ class GaussianDiffusion:
             with torch.no_grad():
                 out = self._step(kind, model, img, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, nz,
                                  seed, k, eta, offset)
+            if k == len(indices) - 1:
+                check_model_range(model, device)   # once per loop: one stream sync
             yield out
             img = out["sample"]
 

@@ -37,8 +37,8 @@ import functools
 import torch
 
 from .. import _lib
-from ..gaussian_diffusion import (LossType, ModelMeanType, ModelVarType, STEP_DDIM, STEP_DDPM, fresh_seed,
-                                  get_named_beta_schedule)
+from ..gaussian_diffusion import (LossType, ModelMeanType, ModelVarType, STEP_DDIM, STEP_DDPM, check_model_range,
+                                  fresh_seed, get_named_beta_schedule)
 from ..respace import SpacedDiffusion, space_timesteps
 from .condition_methods import Identity, PosteriorSampling
 
@@ -124,6 +124,7 @@ class _GuidedSampler(SpacedDiffusion):
         for k, i in enumerate(indices):
             nz = None if step_noise is None else step_noise[k]
             x = self._guided_step(model, x, i, measurement, method, nz, seed, k, sample_offset, self.distances[k])[0]
+        check_model_range(model, x.device)
         return x
 
     def p_sample_step(self, model, x, index, measurement, measurement_cond_fn, noise=None, seed=None, counter=0,

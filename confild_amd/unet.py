@@ -302,6 +302,32 @@ class UNetModel(nn.Module):
                                                 ws.numel(), _lib.stream_of(x.device)), "cfd_unet_forward")
         return eps
 
+    def check_finite(self, device=None):
+        """Range guard of the split-f16 convolutions: reads and clears the device flag
+        that every forward's last convolution raises on a non-finite eps (an
+        activation beyond the f16 range, 65504, becomes inf in the f16 hi part).
+        Raises CfdError in split_f16 compute (the fp32 / bf16 modes have no such
+        range; there a non-finite eps only warns).  Synchronises the stream; the
+        samplers call it once per loop."""
+        import warnings
+        dev = torch.device(device) if device is not None else next(self.parameters()).device
+        if dev.type != "cuda":
+            return True
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        entry = self._handles.get(idx)
+        if entry is None:
+            return True
+        flag = C.c_int(0)
+        _lib.check(_lib.load().cfd_unet_check_finite(entry[0], C.byref(flag), _lib.stream_of(dev)),
+                   "cfd_unet_check_finite")
+        if not flag.value:
+            return True
+        if self.compute == "split_f16":
+            raise _lib.CfdError("U-Net produced a non-finite eps in split_f16 compute: an activation exceeded the f16 "
+                                "range (65504) of the split convolutions; run with set_compute('fp32')")
+        warnings.warn(f"U-Net produced a non-finite eps ({self.compute} compute)", RuntimeWarning, stacklevel=2)
+        return False
+
     # -- input-gradient (DPS adjoint) ---------------------------------------------
     def forward_tape(self, x: torch.Tensor, timesteps: torch.Tensor) -> torch.Tensor:
         """forward() that also records the activations for input_vjp (bit-identical eps)."""

@@ -92,6 +92,13 @@ int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
 int  cfd_unet_set_compute(cfd_unet* h, int compute);
 int  cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                       void* workspace, size_t ws_bytes, void* stream);
+/* Range guard of the split-f16 compute (no reference counterpart: the
+ * reference's fp32 aten ops have no f16 range).  Every forward's last
+ * convolution raises a device flag when an eps value is not finite -- an
+ * activation beyond 65504 makes its f16 hi part infinite and reaches eps as
+ * inf / NaN.  Reads the flag accumulated since the previous call (stream-
+ * ordered, synchronises `stream`) into *nonfinite and clears it. */
+int  cfd_unet_check_finite(cfd_unet* h, int* nonfinite, void* stream);
 
 /* Input-gradient of the U-Net (DPS adjoint; replaces the autograd.grad of
  * grad_and_value through UNetModel.forward, C/src/guided_diffusion/

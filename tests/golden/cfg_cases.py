@@ -70,3 +70,70 @@ def case4_files(tmp: str) -> dict:
     sd = synth.siren_state_dict(s, 3, 384, 3, 15, 384)
     torch.save({"epoch": 20000, "model_state_dict": {k: T(v) for k, v in sd.items()}}, paths["ckpt"])
     return paths
+
+
+# CNF_inference (N/cnf/inference_function.py:79-304) on a trained-checkpoint
+# directory: (name, dims, lumped, is_pub, SIREN (d, L, c, nh, H), data shape,
+# latent count, predict indices)
+CNF_INF = {
+    "grid2d": dict(dims=2, lumped=False, is_pub=False, siren=(2, 16, 3, 2, 32), data_shape=(7, 12, 10, 3),
+                   n_lat=7, idx=[0, 3, 5, 6], seed=31),
+    "lumped3d_pub": dict(dims=3, lumped=True, is_pub=True, siren=(3, 24, 3, 3, 64), data_shape=(9, 300, 3),
+                         n_lat=9, idx=[8, 1, 4], seed=32),
+}
+
+# the Case4 notebook's post-processing (cells 26-32): decoder over the masked
+# points, rearrange, ReconstructFrame into the infos.npz Mask grid
+POST = dict(siren=(3, 16, 3, 2, 32), grid=(8, 6, 5), s=2, t=3, seed=41)
+
+
+def cnf_inference_files(tmp: str, name: str) -> dict:
+    """checkpoint dir (checkpoint_*.pt + normalizer_params.pt), config YAML and a
+    data .npy for CNF_inference, from synth seeds."""
+    import yaml
+    c = CNF_INF[name]
+    d, L, co, nh, H = c["siren"]
+    s = c["seed"]
+    T = torch.from_numpy
+    ck = os.path.join(tmp, "ckpt")
+    os.makedirs(ck, exist_ok=True)
+    sd = {k: T(v) for k, v in synth.siren_state_dict(s, d, L, co, nh, H).items()}
+    lat = T(synth.normal(s, "cnfinf/latents", (c["n_lat"], L)) * np.float32(0.5))
+    hidden = lat if c["is_pub"] else {"latents": lat}
+    torch.save({"epoch": 5, "model_state_dict": sd, "hidden_states": hidden}, os.path.join(ck, "checkpoint_5.pt"))
+    npts = int(np.prod(c["data_shape"][1:-1]))
+    yshape = (1, npts, co) if c["lumped"] else (1, co)
+    torch.save({"x_normalizer_params": (T(synth.uniform(s, "cnfinf/xhi", (1, d), 1.0, 1.5)),
+                                        T(synth.uniform(s, "cnfinf/xlo", (1, d), -0.5, 0.0))),
+                "y_normalizer_params": (T(synth.uniform(s, "cnfinf/yhi", yshape, 0.5, 2.0)),
+                                        T(-synth.uniform(s, "cnfinf/ylo", yshape, 0.5, 2.0)))},
+               os.path.join(ck, "normalizer_params.pt"))
+    cfg = {"dims": c["dims"], "lumped_latent": c["lumped"], "hidden_size": L,
+           "NF": {"name": "SIRENAutodecoder_film", "in_coord_features": d, "out_features": co,
+                  "num_hidden_layers": nh, "hidden_features": H}}
+    with open(os.path.join(tmp, "cnf.yml"), "w") as f:
+        yaml.safe_dump(cfg, f)
+    np.save(os.path.join(tmp, "data.npy"), synth.uniform(s, "cnfinf/data", c["data_shape"], -1.0, 1.0))
+    return dict(checkpoint=os.path.join(ck, "checkpoint_5.pt"), config=os.path.join(tmp, "cnf.yml"),
+                data=os.path.join(tmp, "data.npy"))
+
+
+def cnf_inference_coords(name: str) -> np.ndarray:
+    c = CNF_INF[name]
+    d = c["siren"][0]
+    return synth.uniform(c["seed"], "cnfinf/coords", tuple(c["data_shape"][1:-1]) + (d,), 0.0, 1.0)
+
+
+def post_inputs():
+    """Mask grid, masked coordinates, (s*t, L) latents and normaliser bounds."""
+    c = POST
+    d, L, co, nh, H = c["siren"]
+    s = c["seed"]
+    mask = synth.uniform(s, "post/mask", c["grid"], 0.0, 1.0) < 0.55
+    n = int(mask.sum())
+    coords = synth.uniform(s, "post/coords", (n, d), 0.0, 1.0)
+    lat = synth.normal(s, "post/lat", (c["s"] * c["t"], L)) * np.float32(0.5)
+    xhi, xlo = np.ones((1, d), np.float32), np.zeros((1, d), np.float32)
+    yhi = synth.uniform(s, "post/yhi", (co,), 0.5, 2.0)
+    ylo = -synth.uniform(s, "post/ylo", (co,), 0.5, 2.0)
+    return mask, coords, lat, xhi, xlo, yhi, ylo

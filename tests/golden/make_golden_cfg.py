@@ -59,7 +59,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from confild_amd import synth  # noqa: E402
-from cfg_cases import CASE4_OP, CFG_A, DPS_D, TRAJ_B, case4_files, noise_for, unet_weights  # noqa: E402
+from cfg_cases import (CASE4_OP, CFG_A, CNF_INF, DPS_D, POST, TRAJ_B, case4_files, cnf_inference_coords,  # noqa: E402
+                       cnf_inference_files, noise_for, post_inputs, unet_weights)
 
 torch.set_num_threads(8)
 
@@ -281,7 +282,54 @@ def gen_case4dps():
           nparams=np.int64(sum(int(np.prod(s)) for s in shapes.values())))
 
 
-GEN = {"trajB": gen_trajB, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps}
+# ---------------------------------------------------------------------------
+def gen_cnfinf():
+    """CNF_inference (inference_function.py:79-304): normal and is_pub checkpoints,
+    predict on given indices, create_coordinates_grid from the data shape."""
+    from ConditionalNeuralField.cnf.inference_function import CNF_inference
+    out = {}
+    for name in CNF_INF:
+        with tempfile.TemporaryDirectory() as tmp:
+            f = cnf_inference_files(tmp, name)
+            inf = CNF_inference(checkpoint_path=f["checkpoint"], config_path=f["config"], data_path=f["data"],
+                                device="cpu", is_pub=CNF_INF[name]["is_pub"])
+            coords = torch.from_numpy(cnf_inference_coords(name))
+            pred = inf.predict(coords, CNF_INF[name]["idx"], batch_size=2)
+            out[f"{name}_pred"] = pred.numpy()
+            out[f"{name}_grid"] = inf.create_coordinates_grid().numpy()
+            out[f"{name}_grid_shape"] = inf.create_coordinates_grid(
+                tuple(CNF_INF[name]["data_shape"][1:-1])[:3] if len(CNF_INF[name]["data_shape"]) > 3
+                else (5, 4)).numpy()
+            lat_one = inf.latents(torch.LongTensor([1, 2]))
+            out[f"{name}_latent_shape"] = np.array(lat_one.shape, dtype=np.int64)
+    _save("golden_cnfinf.npz", **out)
+
+
+def gen_post():
+    """The Case4 notebook's decode + ReconstructFrame (cells 26-32) at small scale."""
+    from cnf.inference_function import ReconstructFrame, decoder
+    from cnf.nf_networks import SIRENAutodecoder_film
+    from cnf.utils.normalize import Normalizer_ts
+    from einops import rearrange
+    c = POST
+    d, L, co, nh, H = c["siren"]
+    mask, coords, lat, xhi, xlo, yhi, ylo = post_inputs()
+    nf = SIRENAutodecoder_film(d, L, co, nh, H)
+    nf.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(c["seed"], d, L, co, nh,
+                                                                                   H).items()})
+    xn = Normalizer_ts(method="-11", dim=0, params=(torch.from_numpy(xhi), torch.from_numpy(xlo)))
+    yn = Normalizer_ts(method="-11", dim=0, params=(torch.from_numpy(yhi), torch.from_numpy(ylo)))
+    fields = decoder(torch.from_numpy(coords), torch.from_numpy(lat), nf, xn, yn, batch_size=4, device="cpu")
+    fields = rearrange(fields, "(s t) co c -> s t co c", t=c["t"])
+    frames = [ReconstructFrame(fields[ss, kk].numpy(), mask=mask, shape=c["grid"], fill_value=0.)
+              for ss in range(c["s"]) for kk in range(c["t"])]
+    frames = rearrange(np.stack(frames), "(s t) x y z c -> s t x y z c", t=c["t"])
+    nanf = ReconstructFrame(fields[0, 0].numpy(), mask=mask, shape=c["grid"])   # default fill: NaN
+    _save("golden_post.npz", frames=frames.astype(np.float32), nan_frame=nanf.astype(np.float32))
+
+
+GEN = {"trajB": gen_trajB, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps,
+       "cnfinf": gen_cnfinf, "post": gen_post}
 
 if __name__ == "__main__":
     print("torch", torch.__version__)

@@ -202,3 +202,47 @@ def test_case4_real_shape_dps_step(hip, tmp_path):
     print(f"Case4 384^2 DPS step {idx}: x0 {e_x0:.2e}, img {e_img:.2e}, norm {ed:.2e}")
     assert e_x0 <= 2e-5 and e_img <= 2e-5 and ed <= 1e-5
     os.remove(ema)
+
+
+@pytest.mark.parametrize("name", ["grid2d", "lumped3d_pub"])
+def test_cnf_inference_predict_vs_reference(hip, tmp_path, name):
+    """CNF_inference.predict on the fused decoder against the reference's predict
+    of the same checkpoint directory (2-D grid latents; lumped is_pub latents)."""
+    from cfg_cases import CNF_INF, cnf_inference_coords, cnf_inference_files
+    from confild_amd.inference_function import CNF_inference
+    c = CNF_INF[name]
+    g = golden("golden_cnfinf.npz")
+    f = cnf_inference_files(str(tmp_path), name)
+    inf = CNF_inference(f["checkpoint"], f["config"], f["data"], device="cuda", is_pub=c["is_pub"])
+    pred = inf.predict(torch.from_numpy(cnf_inference_coords(name)), c["idx"], batch_size=2)
+    err = _rel(pred, g[f"{name}_pred"])
+    print(f"CNF_inference {name}: {err:.2e}")
+    assert pred.shape == g[f"{name}_pred"].shape and err <= 2e-5
+    allp = inf.get_all_predictions(torch.from_numpy(cnf_inference_coords(name)))
+    assert torch.equal(allp[c["idx"]], pred)
+
+
+def test_case4_postprocessing_chain_vs_reference(hip):
+    """The notebook's cells 26-32: decoder over the masked points, rearrange
+    "(s t) co c -> s t co c", ReconstructFrame of every frame into the Mask grid."""
+    from cfg_cases import POST, post_inputs
+    from einops import rearrange
+    from confild_amd.inference_function import ReconstructFrame, decoder
+    g = golden("golden_post.npz")
+    d, L, co, nh, H = POST["siren"]
+    mask, coords, lat, xhi, xlo, yhi, ylo = post_inputs()
+    nf = SIRENAutodecoder_film(d, L, co, nh, H)
+    nf.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(POST["seed"], d, L, co, nh,
+                                                                                   H).items()})
+    nf.to(DEV)
+    T = torch.from_numpy
+    xn = Normalizer_ts(method="-11", dim=0, params=(T(xhi), T(xlo)))
+    yn = Normalizer_ts(method="-11", dim=0, params=(T(yhi), T(ylo)))
+    fields = decoder(T(coords).to(DEV), T(lat).to(DEV), nf, xn, yn, batch_size=4, device=DEV)
+    fields = rearrange(fields, "(s t) co c -> s t co c", t=POST["t"])
+    frames = np.stack([ReconstructFrame(fields[s, t].numpy(), mask=mask, shape=POST["grid"], fill_value=0.)
+                       for s in range(POST["s"]) for t in range(POST["t"])])
+    frames = rearrange(frames, "(s t) x y z c -> s t x y z c", t=POST["t"])
+    err = _rel(frames, g["frames"])
+    assert frames.shape == g["frames"].shape and err <= 2e-5, err
+    assert np.array_equal(frames[..., 0][:, :, ~mask], np.zeros_like(frames[..., 0][:, :, ~mask]))

@@ -4,8 +4,8 @@ exact fp32 kernels, on the reference-pinned fixture inputs.
 
 The claim under test: split-f16 is an fp32-accuracy U-Net -- its error against
 fp64 is bounded by 2x the error of the fp32 HIP path (and of the fp32 CPU
-oracle) plus 1e-7 of the output scale, and it meets the 1e-4 tolerance of the
-fp32 parity tests against the reference fixtures.
+oracle) plus 1e-7 of the output scale, and it meets the tolerance of the
+fp32 parity tests against the reference fixtures (1e-5).
 """
 import ast
 
@@ -47,7 +47,7 @@ def test_split_unet_has_fp32_accuracy(hip, name):
           f"cpu-fp32 {e_cpu.max() / scale:.3e}; mean split {esp.mean() / scale:.3e} fp32 {e32.mean() / scale:.3e}")
     assert esp.max().item() <= 2 * max(e32.max().item(), e_cpu.max().item()) + 1e-7 * scale
     assert esp.mean().item() <= 2 * max(e32.mean().item(), e_cpu.mean().item()) + 1e-8 * scale
-    assert np.abs(out["split_f16"].numpy() - g["eps"]).max() / np.abs(g["eps"]).max() <= 1e-4
+    assert np.abs(out["split_f16"].numpy() - g["eps"]).max() / np.abs(g["eps"]).max() <= 1e-5
 
 
 def test_split_unet_batch_invariant(hip):
@@ -62,3 +62,31 @@ def test_split_unet_batch_invariant(hip):
     eps = m(x, t)
     for i in (0, 3):
         assert torch.equal(m(x[i:i + 1], t[i:i + 1]), eps[i:i + 1])
+
+
+def test_split_range_guard_raises_beyond_f16_range(hip):
+    """Activations beyond 65504 make a split-f16 hi part infinite.  With the first
+    convolution's weights scaled by 1e5, the raw residual stream the Downsample
+    and skip convolutions read (no GroupNorm in front) leaves the f16 range: the
+    split-f16 sampler must raise (UNetModel.check_finite, once per loop) while
+    the exact fp32 path stays finite.  Unscaled weights pass the guard."""
+    from confild_amd import _lib
+    from confild_amd.script_util import create_gaussian_diffusion
+    g = golden("unet_tiny16.npz")
+    kw = ast.literal_eval(str(g["kwargs"]))
+    m = create_model(**kw)
+    sd = synth.unet_state_dict(int(g["seed"]), {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.to(DEV).set_compute("split_f16")
+    d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="3")
+    x = d.p_sample_loop(m, (2, 1, 16, 16), seed=5)
+    assert torch.isfinite(x).all() and m.check_finite()
+    big = {k: v.clone() for k, v in m.state_dict().items()}
+    big["input_blocks.0.0.weight"] *= 1e5
+    m.load_state_dict(big)
+    with pytest.raises(_lib.CfdError, match="f16"):
+        d.p_sample_loop(m, (2, 1, 16, 16), seed=5)
+    m.set_compute("fp32")
+    x32 = d.p_sample_loop(m, (2, 1, 16, 16), seed=5)
+    eps = m(torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["t"]).to(DEV))
+    assert torch.isfinite(x32).all() and torch.isfinite(eps).all() and m.check_finite()

@@ -193,3 +193,58 @@ def test_single_step_default_noise_is_fresh():
     assert a != b
     assert gd.fresh_seed(torch.zeros(1), None) == 0
     assert gd.fresh_seed(None, 7) == 7
+
+
+def _cfg_cases():
+    import sys
+    from conftest import GOLDEN
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    import cfg_cases
+    return cfg_cases
+
+
+@pytest.mark.parametrize("name", ["grid2d", "lumped3d_pub"])
+def test_cnf_inference_host_side_matches_reference(tmp_path, name):
+    """CNF_inference (inference_function.py:79-304) on CPU: checkpoint / normaliser /
+    YAML loading, the is_pub remap of a bare latent tensor, LatentContainer's
+    expand dims and create_coordinates_grid, against the reference's own run."""
+    from confild_amd.inference_function import CNF_inference
+    cc = _cfg_cases()
+    c = cc.CNF_INF[name]
+    g = golden("golden_cnfinf.npz")
+    f = cc.cnf_inference_files(str(tmp_path), name)
+    inf = CNF_inference(f["checkpoint"], f["config"], f["data"], device="cpu", is_pub=c["is_pub"])
+    assert np.array_equal(inf.create_coordinates_grid().numpy(), g[f"{name}_grid"])
+    shape = tuple(c["data_shape"][1:-1])[:3] if len(c["data_shape"]) > 3 else (5, 4)
+    assert np.array_equal(inf.create_coordinates_grid(shape).numpy(), g[f"{name}_grid_shape"])
+    assert tuple(inf.latents(torch.LongTensor([1, 2])).shape) == tuple(g[f"{name}_latent_shape"])
+    ck = torch.load(f["checkpoint"], weights_only=True)
+    lat = ck["hidden_states"] if c["is_pub"] else ck["hidden_states"]["latents"]
+    assert torch.equal(inf.latents.latents.detach(), lat)
+    with pytest.raises(_lib.CfdError):      # no CPU fallback for the decode itself
+        inf.predict(torch.from_numpy(cc.cnf_inference_coords(name)), [0])
+    with pytest.raises(FileNotFoundError):
+        CNF_inference(f["checkpoint"] + ".missing", f["config"], f["data"], device="cpu")
+    if not c["is_pub"]:   # no latent codes in hidden_states (inference_function.py:185-187)
+        torch.save({**ck, "hidden_states": {}}, f["checkpoint"])
+        with pytest.raises(ValueError):
+            CNF_inference(f["checkpoint"], f["config"], f["data"], device="cpu")
+
+
+def test_reconstruct_frame_matches_reference():
+    """ReconstructFrame (inference_function.py:15-19): scatter of masked points
+    into the infos.npz Mask grid, zero and default-NaN fill, as the reference
+    produced them in the Case4 notebook's post-processing chain (golden_post)."""
+    from confild_amd.inference_function import ReconstructFrame
+    cc = _cfg_cases()
+    g = golden("golden_post.npz")
+    mask = cc.post_inputs()[0]
+    fr = g["frames"]
+    for s in range(fr.shape[0]):
+        for t in range(fr.shape[1]):
+            out = ReconstructFrame(fr[s, t][mask], mask=mask, shape=cc.POST["grid"], fill_value=0.)
+            assert np.array_equal(out.astype(np.float32), fr[s, t])
+    nanf = ReconstructFrame(g["nan_frame"][mask], mask=mask, shape=cc.POST["grid"])
+    assert np.array_equal(np.isnan(nanf), np.isnan(g["nan_frame"]))
+    assert np.array_equal(nanf[mask].astype(np.float32), g["nan_frame"][mask])
