@@ -369,7 +369,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     float* h1 = ws.take((size_t)B * h->tdim);
     float* emb = ws.take((size_t)B * h->tdim);
     float* embo = ws.take((size_t)B * h->emb_total);
-    double* gnpart = (double*)ws.take((size_t)B * 64 * 32 * 2 * 2);
+    double* gnpart = (double*)ws.take((size_t)B * cfd::kGnMaxChunks * 32 * 2 * 2);
     float* gnss = ws.take((size_t)B * 1024 * 2);
     // normalised (+SiLU) input of the next conv (widest: an output block's concat)
     float* nbuf = ws.take((size_t)B * z.max_cat);
@@ -652,7 +652,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     const Sizes z = sizes(h);
     const size_t kSplitCap = split_cap(B);
     float* splitk = ws.take(kSplitCap);
-    double* gnpart = (double*)ws.take((size_t)B * 64 * 32 * 2 * 2);
+    double* gnpart = (double*)ws.take((size_t)B * cfd::kGnMaxChunks * 32 * 2 * 2);
     float* gnfin = ws.take((size_t)B * 64);
     float* gpool[4];
     for (auto& p : gpool) p = ws.take((size_t)B * z.max_cat);

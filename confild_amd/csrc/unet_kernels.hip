@@ -547,14 +547,24 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             if (m < a.M) {
                 const int b = m / HWo, rem = m - b * HWo;
                 const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
-                int iy = (a.up ? oy - a.pad : oy * a.stride - a.pad) + ty;
-                int ix = (a.up ? ox - a.pad : ox * a.stride - a.pad) + tx;
+                int iy, ix;
                 bool ok;
-                if (a.up) {
+                if (TMODE) {   // transposed addressing: dY[(o + pad - tap) / s] where divisible
+                    iy = oy + a.pad - ty;
+                    ix = ox + a.pad - tx;
+                    ok = iy >= 0 && ix >= 0 && ((iy | ix) & smask) == 0;
+                    iy >>= sshift;
+                    ix >>= sshift;
+                    ok = ok && iy < a.Hin && ix < a.Win;
+                } else if (a.up) {
+                    iy = oy - a.pad + ty;
+                    ix = ox - a.pad + tx;
                     ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
                     iy >>= 1;
                     ix >>= 1;
                 } else {
+                    iy = oy * a.stride - a.pad + ty;
+                    ix = ox * a.stride - a.pad + tx;
                     ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
                 }
                 if (ok) pix = (b * a.Hin + iy) * a.Win + ix;
@@ -1263,7 +1273,14 @@ __global__ void linear_kernel(const float* __restrict__ x, const float* __restri
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-int gn_chunks(int HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 16)); }
+// Pixel chunks of the three-kernel GroupNorm (forward and backward): a function
+// of HW only (batch invariance).  Up to 64 at the config-B sizes; the large
+// latents (Case4 384^2, 192^2) take up to kGnMaxChunks so a batch-1 sample still
+// spreads its statistics pass over the whole chip.
+int gn_chunks(int HW) {
+    const int64_t small = std::min<int64_t>(64, HW / 16);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(kGnMaxChunks, std::max<int64_t>(HW / 64, small)));
+}
 
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
@@ -1287,9 +1304,12 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     a.B = B;
     CFD_REQUIRE(!a.kpart || gn_takes_splitk(a, B), CFD_ESTATE, "internal: split-K source on a GroupNorm path without it");
     static const int fused = env_int("CFD_GN_FUSED", 1);
-    if (fused && a.Ctot % 128 == 0) {
-        const int nq = a.Ctot / 128, rows = 512 / nq;
-        const int ipt = (int)ceil_div(a.HW, rows);
+    static const int big = env_int("CFD_GN_BIG", 1);   // 0: the one-launch kernels at every size
+    const int ipt = a.Ctot % 128 == 0 ? (int)ceil_div(a.HW, 512 / (a.Ctot / 128)) : 0;
+    // large latents (ipt > 32): a workgroup per (sample, group) would leave the
+    // chip idle at small batch (32 workgroups at B = 1, 384^2), so they take the
+    // three-kernel path below, whose statistics spread over gn_chunks(HW) chunks
+    if (fused && a.Ctot % 128 == 0 && !(big && ipt > 32 && fused != 2)) {
         const dim3 grid((unsigned)(32 * B));
         if (fused == 2 || ipt > 32)
             hipLaunchKernelGGL(gn_fused_kernel, grid, dim3(256), 0, st, a);
@@ -1363,9 +1383,7 @@ static void launch_conv_tiles_(const ConvArgs& a, const ConvPlan& p, dim3 grid, 
 
 template <bool TMODE, int MODE>
 static void launch_conv_tiles(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-    if constexpr (!TMODE) {
-        if (a.bufaddr) return launch_conv_tiles_<false, MODE, true>(a, p, grid, st);
-    }
+    if (a.bufaddr) return launch_conv_tiles_<TMODE, MODE, true>(a, p, grid, st);
     launch_conv_tiles_<TMODE, MODE, false>(a, p, grid, st);
 }
 
@@ -1391,7 +1409,7 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer
     {   // 32-bit buffer offsets and 24-bit pixel indices must hold
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
         const int64_t wes = (a.wbf || a.wlo) ? 2 : 4;
-        b.bufaddr = bufaddr && !a.tmode && a.ks * a.ks <= 9 && srows < (1 << 24) &&
+        b.bufaddr = bufaddr && a.ks * a.ks <= 9 && srows < (1 << 24) &&
                     srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * wes < (1ll << 31);
     }
     const ConvArgs& a_ = b;

@@ -100,6 +100,7 @@ struct ConvPlan {
     int nw = 4;  // waves per workgroup (8: BM = BN = 128 only)
 };
 
+constexpr int kGnMaxChunks = 512;
 int gn_chunks(int HW);
 // GroupNorm statistics + normalise (+SiLU) into a.out
 void launch_gn(const GnArgs& a, int B, hipStream_t st);
