@@ -35,6 +35,16 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int xswz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
+// hi = f16(x) (RNE, packed convert), lo = f16(x - hi) by v_fma_mix, 4 values
+__device__ __forceinline__ void split4_mix_x(const f4& x, uint2& hi, uint2& lo) {
+    hi.x = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){x[0], x[1]}, h2));
+    hi.y = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){x[2], x[3]}, h2));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.x) : "v"(x[0]), "v"(hi.x));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.x) : "v"(x[1]), "v"(hi.x));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.y) : "v"(x[2]), "v"(hi.y));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.y) : "v"(x[3]), "v"(hi.y));
+}
+
 template <int BM, int BN, int WGM, int WGN, int KG>
 __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs a) {
     constexpr int NW = WGM * WGN * KG, NT = 64 * NW;
@@ -66,58 +76,77 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     const int m0 = bx * BM, n0 = by * BN;
     const int HWo = a.Hout * a.Wout;
     const int kq = tid & 7, rsub = tid >> 3;
+    __shared__ int pixtab[9 * BM];   // source pixel of (tap, tile row), -1: padding
 
-    // staged row-slices: A (pixel m, group g), B (output channel n, group g)
-    int a_b[AIT], a_oy[AIT], a_ox[AIT], a_g[AIT], a_row[AIT];
-    bool a_ok[AIT];
+    // buffer resources (32-bit offsets; launch_conv_x checks they fit)
+    const int srows = a.Hin * a.Win * (a.M / HWo);
+    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
+    {
+        const int ntap = a.ks * a.ks;
+        for (int e = tid; e < ntap * BM; e += NT) {
+            const int tap = e / BM, r = e - tap * BM;
+            const int ty = tap / a.ks, tx = tap - ty * a.ks;
+            const int m = m0 + r;
+            int pix = -1;
+            if (m < a.M) {
+                const int b = m / HWo, rem = m - b * HWo;
+                const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+                int iy, ix;
+                bool ok;
+                if (a.up) {
+                    iy = oy - a.pad + ty;
+                    ix = ox - a.pad + tx;
+                    ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                    iy >>= 1;
+                    ix >>= 1;
+                } else {
+                    iy = oy * a.stride - a.pad + ty;
+                    ix = ox * a.stride - a.pad + tx;
+                    ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+                }
+                if (ok) pix = (b * a.Hin + iy) * a.Win + ix;
+            }
+            pixtab[e] = pix;
+        }
+    }
+
+    // staged row-slices: A (tile row, group g), B (output channel, group g)
+    int a_g[AIT], a_row[AIT], a_m[AIT];
 #pragma unroll
     for (int it = 0; it < AIT; ++it) {
         const int rs = rsub + it * RPP;
         a_g[it] = rs / BM;
         a_row[it] = rs;
-        const int m = m0 + rs % BM;
-        a_ok[it] = m < a.M;
-        const int mm = a_ok[it] ? m : 0;
-        a_b[it] = mm / HWo;
-        const int rem = mm - a_b[it] * HWo;
-        const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
-        if (!a.up) {
-            a_oy[it] = oy * a.stride - a.pad;
-            a_ox[it] = ox * a.stride - a.pad;
-        } else {
-            a_oy[it] = oy - a.pad;
-            a_ox[it] = ox - a.pad;
-        }
+        a_m[it] = rs % BM;
     }
-    const unsigned short* wrow_h[BIT];
-    const unsigned short* wrow_l[BIT];
     int b_g[BIT], b_row[BIT];
-    bool b_ok[BIT];
+    unsigned b_voff[BIT];
 #pragma unroll
     for (int it = 0; it < BIT; ++it) {
         const int rs = rsub + it * RPP;
         b_g[it] = rs / BN;
         b_row[it] = rs;
         const int n = n0 + rs % BN;
-        b_ok[it] = n < a.Cout;
-        wrow_h[it] = (const unsigned short*)a.wbf + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
-        wrow_l[it] = (const unsigned short*)a.wlo + (int64_t)(b_ok[it] ? n : 0) * a.K + 4 * kq;
+        b_voff[it] = n < a.Cout ? (unsigned)((n * a.K + 4 * kq) * 2) : 0x80000000u;
     }
 
     const int nkt = a.K / 32;
     const int per = (nkt + gridDim.z - 1) / gridDim.z;
     const int kt0 = bz * per;
     const int kt1 = min(nkt, kt0 + per);
-    // per-group K position (tap dy, dx and channel base) of tile kt0 + g, advanced by KG tiles
-    int cbg[KG], dyg[KG], dxg[KG];
+    // per-group K position (tap, channel base) of tile kt0 + g, advanced by KG tiles
+    int cbg[KG], tpg[KG];
 #pragma unroll
     for (int g = 0; g < KG; ++g) {
         const int kb = (kt0 + g) * 32;
-        const int tap = kb / a.Ctot;
-        cbg[g] = kb - tap * a.Ctot;
-        dyg[g] = tap / a.ks;
-        dxg[g] = tap - dyg[g] * a.ks;
+        tpg[g] = kb / a.Ctot;
+        cbg[g] = kb - tpg[g] * a.Ctot;
     }
+    __syncthreads();   // pixtab
 
     f4 ra[AIT];
     uint2 rbh[BIT], rbl[BIT];
@@ -125,45 +154,28 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             const int g = a_g[it];
-            const int c0 = cbg[g] + 4 * kq, dy = dyg[g], dx = dxg[g];
-            f4 v = {0.f, 0.f, 0.f, 0.f};
-            int iy, ix;
-            bool ok = a_ok[it] && kt + g < kt1;
-            if (a.up) {
-                iy = a_oy[it] + dy;
-                ix = a_ox[it] + dx;
-                ok = ok && iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
-                iy >>= 1;
-                ix >>= 1;
-            } else {
-                iy = a_oy[it] + dy;
-                ix = a_ox[it] + dx;
-                ok = ok && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-            }
-            if (ok) {
-                const int64_t pix = ((int64_t)a_b[it] * a.Hin + iy) * a.Win + ix;
-                v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0)
-                              : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
-            }
-            ra[it] = v;
+            const int cb = cbg[g];
+            const bool second = cb >= a.C1;
+            const unsigned csrc4 = 4u * (second ? a.C2 : a.C1);
+            const unsigned cofs4 = 4u * ((second ? cb - a.C1 : cb) + 4 * kq);
+            const int pix = kt + g < kt1 ? pixtab[tpg[g] * BM + a_m[it]] : -1;
+            const unsigned off = pix >= 0 ? __umul24((unsigned)pix, csrc4) + cofs4 : 0x80000000u;
+            ra[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(second ? rs2 : rs1, off, 0, 0));
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
             const int g = b_g[it];
-            const bool ok = b_ok[it] && kt + g < kt1;
-            const int64_t koff = (int64_t)(kt + g) * 32;
-            rbh[it] = ok ? *(const uint2*)(wrow_h[it] + koff) : uint2{0u, 0u};
-            rbl[it] = ok ? *(const uint2*)(wrow_l[it] + koff) : uint2{0u, 0u};
+            const unsigned voff = kt + g < kt1 ? b_voff[it] : 0x80000000u;
+            const int soff = (tpg[g] * a.Ctot + cbg[g]) * 2;
+            rbh[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, voff, soff, 0));
+            rbl[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, voff, soff, 0));
         }
 #pragma unroll
         for (int g = 0; g < KG; ++g) {
             cbg[g] += 32 * KG;
             while (cbg[g] >= a.Ctot) {
                 cbg[g] -= a.Ctot;
-                if (++dxg[g] == a.ks) {
-                    dxg[g] = 0;
-                    ++dyg[g];
-                }
+                ++tpg[g];
             }
         }
     };
@@ -171,11 +183,11 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
         char* base = lds + buf * STAGE;
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
-            const h4 hv = __builtin_convertvector(ra[it], h4);
-            const h4 lv = __builtin_convertvector(ra[it] - __builtin_convertvector(hv, f4), h4);
+            uint2 hv, lv;
+            split4_mix_x(ra[it], hv, lv);
             const int off = xswz(a_row[it], kq >> 1) + (kq & 1) * 8;
-            *(h4*)(base + off) = hv;
-            *(h4*)(base + ABYTES + off) = lv;
+            *(uint2*)(base + off) = hv;
+            *(uint2*)(base + ABYTES + off) = lv;
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
@@ -579,10 +591,11 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
     CFD_REQUIRE(a.wbf && a.wlo && !a.tmode, CFD_ESTATE, "conv_x: split-f16 forward only");
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_x needs channels % 32 == 0");
     CFD_REQUIRE(splits == 1 || a.part, CFD_ESTATE, "split-K needs a partial buffer");
-    if (variant >= 10) {   // K1y: 32-bit buffer offsets
+    {   // K1x / K1y: 32-bit buffer offsets, 24-bit pixel indices
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
-        CFD_REQUIRE(srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * 2 < (1ll << 31),
-                    CFD_ESHAPE, "conv_y: operands beyond 2 GiB");
+        CFD_REQUIRE(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) &&
+                        (int64_t)a.Cout * a.K * 2 < (1ll << 31) && a.ks * a.ks <= 9,
+                    CFD_ESHAPE, "conv_x: operands beyond 2 GiB");
     }
     auto grid = [&](int bm, int bn) {
         return dim3((unsigned)ceil_div(a.M, bm), (unsigned)ceil_div(a.Cout, bn), splits);

@@ -1364,6 +1364,25 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // memory guard, on the nominal shape too: part_cap_floats is the slab per 8
     // samples (the caller sizes the real slab as ceil(B/8) of these)
     while (p.splits > 1 && (size_t)p.splits * mn * a.Cout > part_cap_floats) p.splits /= 2;
+    // K1x (conv_x.hip) for the split-f16 3x3 stride-1 convolutions: 64x64 wave
+    // tiles on 32x32x16 MFMAs; 256x128 workgroup tiles where the per-sample shape
+    // has >= 256 pixels at batch 8, 128x128 / 4 waves below (tools/convbench:
+    // 1.04-1.11x / 1.17x the K1s tiles on the config-B shapes, same box)
+    static const int kx = env_int("CFD_CONV_KX", 1);
+    const int64_t srows = mn / ((int64_t)a.Hout * a.Wout) * a.Hin * a.Win;
+    if (kx && a.wbf && a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 &&
+        srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31)) {
+        ConvPlan q;
+        q.kx = mn >= 2048 ? 2 : 1;
+        q.bm = q.kx == 2 ? 256 : 128;
+        q.bn = 128;
+        q.nw = q.kx == 2 ? 8 : 4;
+        const int64_t t = ceil_div(mn, q.bm) * ceil_div(a.Cout, q.bn);
+        q.splits = 1;
+        while (t * q.splits < 256 && nkt / (q.splits * 2) >= 8 && q.splits < 16) q.splits *= 2;
+        while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
+        return q;
+    }
     return p;
 }
 
@@ -1393,7 +1412,16 @@ void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st) {
     check_launch("splitk_reduce_kernel");
 }
 
-int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer) {
+int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defer) {
+    ConvPlan p = p0;
+    if (p.kx >= 0) {   // K1x needs 32-bit operand offsets at the real batch; else K1s tiles, same splits
+        const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
+        if (!(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31))) {
+            p.kx = -1;
+            p.bm = p.bn = 128;
+            p.nw = 8;
+        }
+    }
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
     CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot, CFD_ESHAPE, "conv K mismatch");
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
@@ -1413,6 +1441,11 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer
                     srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * wes < (1ll << 31);
     }
     const ConvArgs& a_ = b;
+    if (p.kx >= 0) {
+        launch_conv_x(a_, p.kx, p.splits, st);
+        if (p.splits > 1 && !defer) launch_splitk_reduce(a, p.splits, st);
+        return p.splits;
+    }
     if (a.tmode && a.wlo)
         launch_conv_tiles<true, 2>(a_, p, grid, st);
     else if (a.tmode)

@@ -98,6 +98,7 @@ struct AttnBwdArgs {
 struct ConvPlan {
     int bm = 128, bn = 128, splits = 1;
     int nw = 4;  // waves per workgroup (8: BM = BN = 128 only)
+    int kx = -1; // >= 0: run the K1x kernel variant (conv_x.hip) instead of conv_gemm_kernel
 };
 
 constexpr int kGnMaxChunks = 512;
