@@ -231,9 +231,8 @@ __global__ __launch_bounds__(256) void gn_fused_kernel(GnArgs a) {
 // loading its IPT float4 at once (the loads pipeline instead of forming a
 // latency chain), summing them, and normalising the same registers (one HBM
 // read instead of two).  Same statistics / order semantics as gn_fused_kernel.
-template <int IPT>
-__global__ __launch_bounds__(512) void gn_fused_reg_kernel(GnArgs a) {
-    constexpr int NT = 512;
+template <int IPT, int NT = 512>
+__global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     const int L = blockIdx.x;
     const int64_t b = L % a.B;
     const int grp = L / a.B;
@@ -1305,6 +1304,7 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     CFD_REQUIRE(!a.kpart || gn_takes_splitk(a, B), CFD_ESTATE, "internal: split-K source on a GroupNorm path without it");
     static const int fused = env_int("CFD_GN_FUSED", 1);
     static const int big = env_int("CFD_GN_BIG", 1);   // 0: the one-launch kernels at every size
+    static const int nt1024 = env_int("CFD_GN_NT1024", 1);
     const int ipt = a.Ctot % 128 == 0 ? (int)ceil_div(a.HW, 512 / (a.Ctot / 128)) : 0;
     // large latents (ipt > 32): a workgroup per (sample, group) would leave the
     // chip idle at small batch (32 workgroups at B = 1, 384^2), so they take the
@@ -1313,6 +1313,12 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
         const dim3 grid((unsigned)(32 * B));
         if (fused == 2 || ipt > 32)
             hipLaunchKernelGGL(gn_fused_kernel, grid, dim3(256), 0, st, a);
+        else if (nt1024 && ipt <= 4)   // 1024 threads: twice the waves (and loads) in flight per CU
+            hipLaunchKernelGGL((gn_fused_reg_kernel<2, 1024>), grid, dim3(1024), 0, st, a);
+        else if (nt1024 && ipt <= 8)
+            hipLaunchKernelGGL((gn_fused_reg_kernel<4, 1024>), grid, dim3(1024), 0, st, a);
+        else if (nt1024 && ipt <= 16)
+            hipLaunchKernelGGL((gn_fused_reg_kernel<8, 1024>), grid, dim3(1024), 0, st, a);
         else if (ipt <= 4)
             hipLaunchKernelGGL(gn_fused_reg_kernel<4>, grid, dim3(512), 0, st, a);
         else if (ipt <= 8)
