@@ -79,7 +79,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     __shared__ int pixtab[9 * BM];   // source pixel of (tap, tile row), -1: padding
 
     // buffer resources (32-bit offsets; launch_conv_x checks they fit)
-    const int srows = a.Hin * a.Win * (a.M / HWo);
+    const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR: a VGPR descriptor field costs a readfirstlane loop per load
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
@@ -143,8 +143,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 #pragma unroll
     for (int g = 0; g < KG; ++g) {
         const int kb = (kt0 + g) * 32;
-        tpg[g] = kb / a.Ctot;
-        cbg[g] = kb - tpg[g] * a.Ctot;
+        tpg[g] = __builtin_amdgcn_readfirstlane(kb / a.Ctot);   // SGPRs: scalar descriptor choice
+        cbg[g] = __builtin_amdgcn_readfirstlane(kb - tpg[g] * a.Ctot);
     }
     __syncthreads();   // pixtab
 
@@ -327,6 +327,256 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 }
 
 // ---------------------------------------------------------------------------
+// K1h: halo-tiled 3x3 stride-1 convolution (optionally on a nearest-2x
+// upsampled input).  A workgroup's BM output pixels are a TR x TW block
+// (TR = BM / TW rows of TW columns, TW dividing the image width) of one sample;
+// per 32-channel chunk it stages the (TR + 2) x (TW + 2) input halo once (split to hi/lo f16 on the way into LDS) and runs the 9 taps
+// as shifted views of it, so an activation is fetched once per chunk instead of
+// once per tap (K1x/K1s gather the 9 im2col rows separately: 4.4x / 5.8x the
+// activation bytes at BM = 128 / 256 on a 64-wide image).  Weights stream per
+// (chunk, tap) through a 2-stage LDS ring.  K order is (chunk, tap) -- the
+// summation order is a function of the per-sample shape only, as K1x's.
+// The next chunk's halo is loaded into registers at tap 0 and written after
+// tap 8 (one extra barrier per chunk), so the halo needs one LDS stage; weight
+// slices are fetched two steps ahead (two register sets, one LDS stage each).
+template <int BM, int TW>
+__global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
+    constexpr int BN = 128, WGM = BM / 64, NT = 64 * WGM * 2;
+    constexpr int TR = BM / TW, HW2 = TW + 2, NPX = (TR + 2) * HW2;
+    constexpr int HPLANE = NPX * 64;                  // one f16 plane of the halo (64 B per pixel)
+    constexpr int HIT = (NPX * 8 + NT - 1) / NT;      // 16-B halo pieces per thread
+    constexpr int BPLANE = BN * 64, BSTAGE = 2 * BPLANE;
+    constexpr int BIT = BN * 4 / NT;                  // 16-B weight pieces per thread and plane
+    static_assert(BM % TW == 0 && BIT >= 1, "tile");
+    __shared__ __attribute__((aligned(16))) char lds[2 * HPLANE + 2 * BSTAGE];
+    char* const halo = lds;
+    char* const ring = lds + 2 * HPLANE;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (a.xcd) {
+        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
+        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
+        bz = Lp % gz;
+        by = (Lp / gz) % gy;
+        bx = Lp / (gz * gy);
+    }
+    const int n0 = by * BN;
+    const int W = a.Wout, HWo = a.Hout * W;
+    // tile bx -> sample, block row, block column (row-major blocks in a sample)
+    const int tps = HWo / BM, tpr = W / TW;
+    const int bimg = bx / tps, tl = bx - bimg * tps;
+    const int y0 = (tl / tpr) * TR, x0 = (tl - (tl / tpr) * tpr) * TW;
+    const int64_t mrow0 = (int64_t)bimg * HWo + (int64_t)y0 * W + x0;   // output pixel of tile position (0, 0)
+
+    const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR: a VGPR descriptor field costs a readfirstlane loop per load
+    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
+
+    // halo pieces of this thread: halo pixel (tid + it*NT) >> 3, channel quad tid & 7
+    const int kq = tid & 7;
+    int hpix[HIT];
+#pragma unroll
+    for (int it = 0; it < HIT; ++it) {
+        const int hp = (tid + it * NT) >> 3;
+        int pix = -1;
+        if (hp < NPX) {
+            const int hr = hp / HW2, hc = hp - hr * HW2;
+            const int iy = y0 - 1 + hr, ix = x0 - 1 + hc;
+            if (iy >= 0 && iy < a.Hout && ix >= 0 && ix < W)
+                pix = a.up ? (bimg * a.Hin + (iy >> 1)) * a.Win + (ix >> 1) : (bimg * a.Hin + iy) * a.Win + ix;
+        }
+        hpix[it] = pix;
+    }
+    // weight pieces: output channel row tid >> 2 (+ NT/4 per it), 16-B chunk tid & 3
+    const int bq = tid & 3;
+    unsigned bvoff[BIT];
+#pragma unroll
+    for (int it = 0; it < BIT; ++it) {
+        const int n = n0 + (tid >> 2) + it * (NT / 4);
+        bvoff[it] = n < a.Cout ? (unsigned)((n * a.K + 8 * bq) * 2) : 0x80000000u;
+    }
+
+    const int nch = a.Ctot / 32;
+    const int per = (nch + gridDim.z - 1) / gridDim.z;
+    const int c0 = bz * per, c1 = min(nch, c0 + per);
+
+    f4 rh[HIT];
+    u4 wx_h[BIT], wx_l[BIT], wy_h[BIT], wy_l[BIT];   // weight slices two steps deep
+    auto load_halo = [&](int c) {
+        const int cb = 32 * c;
+        const bool second = cb >= a.C1;
+        const unsigned csrc4 = 4u * (second ? a.C2 : a.C1);
+        const unsigned cofs4 = 4u * ((second ? cb - a.C1 : cb) + 4 * kq);
+        // one descriptor per branch: a selected descriptor lands in VGPRs and
+        // hipcc wraps every load in a readfirstlane loop
+        if (second) {
+#pragma unroll
+            for (int it = 0; it < HIT; ++it) {
+                const unsigned off = hpix[it] >= 0 ? __umul24((unsigned)hpix[it], csrc4) + cofs4 : 0x80000000u;
+                rh[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs2, off, 0, 0));
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < HIT; ++it) {
+                const unsigned off = hpix[it] >= 0 ? __umul24((unsigned)hpix[it], csrc4) + cofs4 : 0x80000000u;
+                rh[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs1, off, 0, 0));
+            }
+        }
+    };
+    auto store_halo = [&]() {
+#pragma unroll
+        for (int it = 0; it < HIT; ++it) {
+            const int e = tid + it * NT;
+            if (e < NPX * 8) {
+                uint2 hv, lv;
+                split4_mix_x(rh[it], hv, lv);
+                const int off = xswz(e >> 3, kq >> 1) + (kq & 1) * 8;
+                *(uint2*)(halo + off) = hv;
+                *(uint2*)(halo + HPLANE + off) = lv;
+            }
+        }
+    };
+    // step s = (chunk c0 + s / 9, tap s % 9)
+    auto load_w = [&](int s, u4 (&rbh)[BIT], u4 (&rbl)[BIT]) {
+        const int c = c0 + s / 9, t = s % 9;
+        const int soff = (t * a.Ctot + 32 * c) * 2;
+#pragma unroll
+        for (int it = 0; it < BIT; ++it) {
+            rbh[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwh, bvoff[it], soff, 0));
+            rbl[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwl, bvoff[it], soff, 0));
+        }
+    };
+    auto store_w = [&](int stage, const u4 (&rbh)[BIT], const u4 (&rbl)[BIT]) {
+        char* base = ring + stage * BSTAGE;
+#pragma unroll
+        for (int it = 0; it < BIT; ++it) {
+            const int off = xswz((tid >> 2) + it * (NT / 4), bq);
+            *(u4*)(base + off) = rbh[it];
+            *(u4*)(base + BPLANE + off) = rbl[it];
+        }
+    };
+
+    f16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int l32 = lane & 31, hsel = lane >> 5;
+    int hb[2];   // halo pixel of tap (0, 0) for this lane's output pixel, per 32-row block
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int p = wm * 64 + 32 * i + l32;
+        hb[i] = (p / TW) * HW2 + (p % TW);
+    }
+    const int brow0 = wn * 64 + l32;
+    const int nsteps = (c1 - c0) * 9;
+
+    // one step: prefetch the weights of step s + 2, MFMAs of step s on ring stage
+    // s & 1, then park step s + 1's weights (loaded a step ago) in the other stage
+    auto step = [&](int s, u4 (&ldh)[BIT], u4 (&ldl)[BIT], const u4 (&sth)[BIT], const u4 (&stl)[BIT]) {
+        const int c = c0 + s / 9, t = s % 9;
+        if (s + 2 < nsteps) load_w(s + 2, ldh, ldl);
+        if (t == 0 && c + 1 < c1) load_halo(c + 1);   // in registers until this chunk's taps are done
+        const int ty = t / 3;
+        const int tofs = ty * HW2 + (t - 3 * ty);
+        const char* wb = ring + (s & 1) * BSTAGE;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int ch = 2 * s2 + hsel;
+            h8v fah[2], fal[2], fbh[2], fbl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int off = xswz(hb[i] + tofs, ch);
+                fah[i] = *(const h8v*)(halo + off);
+                fal[i] = *(const h8v*)(halo + HPLANE + off);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int off = xswz(brow0 + 32 * j, ch);
+                fbh[j] = *(const h8v*)(wb + off);
+                fbl[j] = *(const h8v*)(wb + BPLANE + off);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        if (s + 1 < nsteps) store_w((s + 1) & 1, sth, stl);
+        __syncthreads();
+        if (t == 8 && s + 1 < nsteps) {   // every wave is past the last tap of chunk c
+            store_halo();
+            __syncthreads();
+        }
+    };
+
+    if (nsteps > 0) {
+        load_w(0, wx_h, wx_l);
+        if (nsteps > 1) load_w(1, wy_h, wy_l);
+        load_halo(c0);
+        store_w(0, wx_h, wx_l);
+        store_halo();
+        __syncthreads();
+        for (int s = 0; s < nsteps; s += 2) {
+            step(s, wx_h, wx_l, wy_h, wy_l);
+            if (s + 1 < nsteps) step(s + 1, wy_h, wy_l, wx_h, wx_l);
+        }
+    }
+
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] *= a.acc_scale;
+    const int n_base = n0 + wn * 64 + l32;
+    const int p_base = wm * 64 + 4 * hsel;   // tile position of acc element 0 of block 0
+    auto pix_of = [&](int p) { return mrow0 + (int64_t)(p / TW) * W + (p % TW); };
+    if (gridDim.z > 1) {
+        float* part = a.part + (int64_t)bz * a.M * a.Cout;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t m = pix_of(p_base + 32 * i + 8 * (e >> 2) + (e & 3));
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int n = n_base + 32 * j;
+                    if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][e];
+                }
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t m = pix_of(p_base + 32 * i + 8 * (e >> 2) + (e & 3));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = n_base + 32 * j;
+                if (n >= a.Cout) continue;
+                float v = a.bias ? acc[i][j][e] + a.bias[n] : acc[i][j][e];
+                if (a.emb) v = v + a.emb[(int64_t)bimg * a.emb_stride + n];
+                if (a.res) v = a.res[(int64_t)m * a.Cout + n] + v;
+                a.out[(int64_t)m * a.Cout + n] = v;
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------
 // K1y: the same GEMM with every operand staged by LDS-DMA into an S-stage LDS
 // ring (buffer_load ... lds: no VGPR staging, S-1 K tiles in flight per
 // workgroup).  The activation tile lands as fp32 (im2col rows gathered per
@@ -428,7 +678,7 @@ __global__ __launch_bounds__(256, 1) void conv_y_kernel(ConvArgs a) {
         const int n = n0 + r;
         b_off[j] = n < a.Cout ? (unsigned)(((int64_t)n * a.K + 8 * c) * 2) : 0x80000000u;
     }
-    const int srows = a.Hin * a.Win * (a.M / HWo);   // input pixels of the whole batch
+    const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR: a VGPR descriptor field costs a readfirstlane loop per load   // input pixels of the whole batch
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
@@ -587,6 +837,18 @@ __global__ __launch_bounds__(256, 1) void conv_y_kernel(ConvArgs a) {
 }
 
 // variant ids (tools/convbench): BM x BN, wave grid, K groups
+// K1h tile width for this shape (0: K1h does not apply): the widest of 64, 32,
+// 16 dividing the image width whose 256-pixel block rows divide the height
+int conv_h_tw(const ConvArgs& a) {
+    const bool geo = !a.tmode && a.ks == 3 && a.stride == 1 && a.pad == 1 && a.C1 % 32 == 0 && a.C2 % 32 == 0 &&
+                     (a.up ? a.Hout == 2 * a.Hin && a.Wout == 2 * a.Win : a.Hout == a.Hin && a.Wout == a.Win) &&
+                     a.M % (a.Hout * a.Wout) == 0;
+    if (!geo) return 0;
+    for (int tw = 64; tw >= 16; tw >>= 1)
+        if (a.Wout % tw == 0 && a.Hout % (256 / tw) == 0) return tw;
+    return 0;
+}
+
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
     CFD_REQUIRE(a.wbf && a.wlo && !a.tmode, CFD_ESTATE, "conv_x: split-f16 forward only");
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_x needs channels % 32 == 0");
@@ -600,6 +862,16 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
     auto grid = [&](int bm, int bn) {
         return dim3((unsigned)ceil_div(a.M, bm), (unsigned)ceil_div(a.Cout, bn), splits);
     };
+    if (variant == 20) {   // K1h, 256-pixel blocks
+        const int tw = conv_h_tw(a);
+        CFD_REQUIRE(tw > 0, CFD_ESHAPE, "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");
+        const dim3 g = grid(256, 128);
+        if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
+        else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
+        check_launch("conv_h_kernel");
+        return splits;
+    }
     switch (variant) {
         case 0: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 2>), grid(128, 128), dim3(512), 0, st, a); break;
         case 1: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1>), grid(128, 128), dim3(256), 0, st, a); break;

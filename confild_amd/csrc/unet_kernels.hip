@@ -498,31 +498,36 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     const int per = (nkt + gridDim.z - 1) / gridDim.z;
     const int kt0 = bz * per;
     const int kt1 = min(nkt, kt0 + per);
-    // wave-uniform K position: (dy, dx) tap and channel base, advanced per tile
-    // in (tap, chunk) order or, with a.korder, (chunk, tap) order: the taps of one
-    // 32-channel chunk back to back re-read activation rows while they are in L2
-    int cb = 0, dy = 0, dx = 0;
-    {
-        const int ntap = a.ks * a.ks;
+    // wave-uniform K position of tile kt: (dy, dx) tap and channel base, in
+    // (tap, chunk) order or, with a.korder, (chunk, tap) order (the taps of one
+    // 32-channel chunk back to back re-read activation rows while they are in
+    // L2).  Derived from kt per tile and pinned to SGPRs: a position carried
+    // across tiles ended up in scratch and VGPRs, and a VGPR-selected buffer
+    // descriptor costs a readfirstlane loop around every load.
+    const int ntap_ = a.ks * a.ks;
+    auto kpos_of = [&](int kt, int& cb, int& dy, int& dx) {
         int tap;
         if (a.korder) {
-            cb = BK * (kt0 / ntap);
-            tap = kt0 - (kt0 / ntap) * ntap;
+            cb = BK * (kt / ntap_);
+            tap = kt - (kt / ntap_) * ntap_;
         } else {
-            const int kb = kt0 * BK;
+            const int kb = kt * BK;
             tap = kb / a.Ctot;
             cb = kb - tap * a.Ctot;
         }
         dy = tap / a.ks;
         dx = tap - dy * a.ks;
-    }
+        cb = __builtin_amdgcn_readfirstlane(cb);
+        dy = __builtin_amdgcn_readfirstlane(dy);
+        dx = __builtin_amdgcn_readfirstlane(dx);
+    };
 
     const int smask = a.stride - 1, sshift = a.stride >> 1;
     f4 ra[AIT], rb[BIT];
     uint2 rbh[BIT], rbl[BIT];
     // buffer-addressed path: resources, per-row weight offsets, the pixel table
     constexpr int WES = (BF || SP) ? 2 : 4;   // weight element bytes
-    const int srows = a.Hin * a.Win * (a.M / HWo);
+    const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR descriptor fields
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
@@ -573,6 +578,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
         __syncthreads();
     }
     auto load_tile = [&](int kt) {
+        int cb, dy, dx;
+        kpos_of(kt, cb, dy, dx);
         const int c0 = cb + 4 * kq;
         const int kpos = (dy * a.ks + dx) * a.Ctot + cb;   // this tile's offset in a (tap, channel) weight row
         if constexpr (BUFA) {
@@ -637,24 +644,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             if constexpr (!BF && !SP)
                 rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kpos) : f4{0.f, 0.f, 0.f, 0.f};
         }
-        }
-        if (a.korder) {
-            if (++dx == a.ks) {
-                dx = 0;
-                if (++dy == a.ks) {
-                    dy = 0;
-                    cb += BK;
-                }
-            }
-        } else {
-            cb += BK;
-            if (cb >= a.Ctot) {
-                cb = 0;
-                if (++dx == a.ks) {
-                    dx = 0;
-                    ++dy;
-                }
-            }
         }
     };
     auto store_tile = [&](int buf) {
@@ -1379,6 +1368,23 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     if (kx && a.wbf && a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 &&
         srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31)) {
         ConvPlan q;
+        // K1h (halo tiles, conv_x.hip) where the image is at least 32x32: each
+        // activation fetched once per 32-channel chunk instead of once per tap
+        // (tools/convbench, same box: 1.19-1.29x K1x on the config-B 64^2/32^2
+        // shapes, 0.94x at 16^2); split-K over the chunks
+        static const int kh = env_int("CFD_CONV_KH", 1);
+        if (kh && (int64_t)a.Hout * a.Wout >= 1024 && conv_h_tw(a) > 0) {
+            q.kx = 20;
+            q.bm = 256;
+            q.bn = 128;
+            q.nw = 8;
+            const int64_t t = ceil_div(mn, 256) * ceil_div(a.Cout, 128);
+            const int nch = a.Ctot / 32;
+            q.splits = 1;
+            while (t * q.splits < 256 && nch / (q.splits * 2) >= 2 && q.splits < 16) q.splits *= 2;
+            while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
+            return q;
+        }
         q.kx = mn >= 2048 ? 2 : 1;
         q.bm = q.kx == 2 ? 256 : 128;
         q.bn = 128;

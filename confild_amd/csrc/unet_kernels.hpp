@@ -118,6 +118,7 @@ void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st);
 // K1x (conv_x.hip): split-f16 forward convolution on 32x32x16 MFMAs with 64x64
 // wave tiles and an in-workgroup K split; variant selects the tile shape
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st);
+int conv_h_tw(const ConvArgs& a);   // K1h tile width for a shape, 0: not applicable
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
 void launch_conv_out(const ConvArgs& a, hipStream_t st);
 void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t st);

@@ -31,6 +31,7 @@
 
 namespace cfd {
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st);
+int conv_h_tw(const ConvArgs& a);
 }
 
 struct Shape {
@@ -49,6 +50,9 @@ static const Shape SHAPES[] = {
     {"L2 conv 384->384", 8, 16, 16, 384, 0, 384, 3, 1, 0},
     {"L3 conv 512->512", 8, 8, 8, 512, 0, 512, 3, 1, 0},
     {"L0 skip1x1 384->128", 8, 64, 64, 256, 128, 128, 1, 1, 0},
+    {"C4 384^2 conv 128->128", 1, 384, 384, 128, 0, 128, 3, 1, 0},
+    {"C4 96^2 conv 256->256", 1, 96, 96, 256, 0, 256, 3, 1, 0},
+    {"C4 48^2 conv 256->256", 1, 48, 48, 256, 0, 256, 3, 1, 0},
 };
 
 static uint16_t f2h(float v) {
@@ -164,12 +168,16 @@ int main(int argc, char** argv) {
         for (int v : variants) {
             const int BMv_[] = {128, 128, 256, 128, 64}, BNv_[] = {128, 128, 128, 64, 128};
             const int vb = v >= 10 ? 0 : v;
-            const int BMv = BMv_[vb], BNv = BNv_[vb];
+            const int BMv = v == 20 ? 256 : BMv_[vb], BNv = BNv_[vb];
+            if (v >= 20 && !cfd::conv_h_tw(a)) continue;
             const int64_t tiles = ((M + BMv - 1) / BMv) * ((s.Cout + BNv - 1) / BNv);
             int splits = splits_x;
             if (!splits) {
                 splits = 1;
-                while (tiles * splits < 256 && K / 32 / (splits * 2) >= 8 && splits < 16) splits *= 2;
+                if (v >= 20)
+                    while (tiles * splits < 256 && Ctot / 32 / (splits * 2) >= 2 && splits < 16) splits *= 2;
+                else
+                    while (tiles * splits < 256 && K / 32 / (splits * 2) >= 8 && splits < 16) splits *= 2;
             }
             cfd::ConvArgs b = a;
             b.out = out1;

@@ -25,7 +25,7 @@ for d in sys.argv[1:]:
             if x["Counter_Name"] in ("SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE", "TCC_HIT_sum", "FETCH_SIZE"):
                 dur[key].append(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]))
 print("%-40s %6s %8s %5s %5s %5s %6s %6s %6s %6s %7s %6s" % ("kernel", "WGs", "us", "wait", "inst", "act", "mfma",
-                                                            "GHz", "v/mf", "l/mf", "L2hit", "MBfet"))
+                                                            "GHz", "v/mf", "l/mf", "L2hit", "MBfet") + "  ldsW  bankc")
 for k in sorted(acc, key=lambda k: (k[0], k[1])):
     d = acc[k]
     g = lambda c: d[c] / max(n[k][c], 1)
@@ -37,4 +37,5 @@ for k in sorted(acc, key=lambda k: (k[0], k[1])):
     hit = g("TCC_HIT_sum") / max(g("TCC_HIT_sum") + g("TCC_MISS_sum"), 1)
     print("%-40s %6d %8.1f %5.2f %5.2f %5.2f %6.3f %6.2f %6.2f %6.2f %7.3f %6.1f" % (
         k[0], k[1], t / 1e3, g("SQ_WAIT_ANY") / wc, g("SQ_WAIT_INST_ANY") / wc, g("SQ_ACTIVE_INST_ANY") / wc, util,
-        cyc / t if t else 0, g("SQ_INSTS_VALU") / m, g("SQ_INSTS_LDS") / m, hit, 2 * g("FETCH_SIZE") / 1e3))
+        cyc / t if t else 0, g("SQ_INSTS_VALU") / m, g("SQ_INSTS_LDS") / m, hit, 2 * g("FETCH_SIZE") / 1e3) +
+        "  %5.2f %5.2f" % (g("SQ_WAIT_INST_LDS") / wc, g("SQ_LDS_BANK_CONFLICT") / max(g("SQ_LDS_IDX_ACTIVE"), 1)))
