@@ -330,31 +330,51 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // K1h: halo-tiled 3x3 stride-1 convolution (optionally on a nearest-2x
 // upsampled input).  A workgroup's BM output pixels are a TR x TW block
 // (TR = BM / TW rows of TW columns, TW dividing the image width) of one sample;
-// per 32-channel chunk it stages the (TR + 2) x (TW + 2) input halo once (split to hi/lo f16 on the way into LDS) and runs the 9 taps
-// as shifted views of it, so an activation is fetched once per chunk instead of
-// once per tap (K1x/K1s gather the 9 im2col rows separately: 4.4x / 5.8x the
-// activation bytes at BM = 128 / 256 on a 64-wide image).  Weights stream per
-// (chunk, tap) through a 2-stage LDS ring.  K order is (chunk, tap) -- the
-// summation order is a function of the per-sample shape only, as K1x's.
-// The next chunk's halo is loaded into registers at tap 0 and written after
-// tap 8 (one extra barrier per chunk), so the halo needs one LDS stage; weight
-// slices are fetched two steps ahead (two register sets, one LDS stage each).
-template <int BM, int TW>
-__global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
-    constexpr int BN = 128, WGM = BM / 64, NT = 64 * WGM * 2;
+// per 32-channel chunk a wave group stages the (TR + 2) x (TW + 2) input halo
+// once (split to hi/lo f16 on the way into LDS) and runs the 9 taps as shifted
+// views of it, so an activation is fetched once per chunk instead of once per
+// tap (K1x/K1s gather the 9 im2col rows separately: 4.4x / 5.8x the activation
+// bytes at BM = 128 / 256 on a 64-wide image).  Weights stream per (chunk, tap)
+// through a 2-stage LDS ring, fetched two steps ahead (two register sets).  The
+// next chunk's halo is loaded into registers at tap 0 and written after tap 8
+// (one extra barrier per chunk), so the halo needs one LDS stage.
+//
+// KG wave groups (BM/32 waves each, own halo and weight ring) take the
+// chunks of the workgroup's range round-robin and meet once through LDS at the
+// end, group 0 adding the others' sums in group order: an in-workgroup K split
+// with no partial slab in HBM (split-K over workgroups, gridDim.z, still
+// composes with it).  K order is (chunk, tap) per group -- every output's
+// summation order is a function of the per-sample shape only, as K1x's.  The
+// planner ships BM = 256, KG = 1: 128-pixel blocks in 2 groups (variant 21)
+// measured 0.83-1.07x of it on the config-B shapes, their weight slices serving
+// half the pixels, so the split-K slab they avoid does not pay for itself.
+//
+// Measured and not kept (tools/convbench): fragment reads software-
+// pipelined across steps (3-stage ring, 2 halo stages): no change; the timing
+// experiments (no global loads / no per-step LDS reads / no barriers / no LDS
+// stores, wrong results) reach 1.0-1.1 / 1.1 / 1.05 / 1.2 / all four 1.3x --
+// the MFMA chain alone runs at ~430 TF fp32-equivalent on random data at the
+// clock the chip holds under it, ~0.52 of the 2.4 GHz split-f16 peak.
+template <int BM, int TW, int KG = 1>
+__global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
+    constexpr int BN = 128, WGM = BM / 64, NTG = 64 * WGM * 2, NT = NTG * KG;   // threads per group / total
     constexpr int TR = BM / TW, HW2 = TW + 2, NPX = (TR + 2) * HW2;
     constexpr int HPLANE = NPX * 64;                  // one f16 plane of the halo (64 B per pixel)
-    constexpr int HIT = (NPX * 8 + NT - 1) / NT;      // 16-B halo pieces per thread
+    constexpr int HIT = (NPX * 8 + NTG - 1) / NTG;    // 16-B halo pieces per thread
     constexpr int BPLANE = BN * 64, BSTAGE = 2 * BPLANE;
-    constexpr int BIT = BN * 4 / NT;                  // 16-B weight pieces per thread and plane
+    constexpr int BIT = BN * 4 / NTG;                 // 16-B weight pieces per thread and plane
+    constexpr int GBYTES = 2 * HPLANE + 2 * BSTAGE;   // one group's halo + weight ring
     static_assert(BM % TW == 0 && BIT >= 1, "tile");
-    __shared__ __attribute__((aligned(16))) char lds[2 * HPLANE + 2 * BSTAGE];
-    char* const halo = lds;
-    char* const ring = lds + 2 * HPLANE;
+    constexpr int RED = (KG - 1) * WGM * 2 * 4 * 16 * 64 * 4;   // parked sums of groups 1..
+    __shared__ __attribute__((aligned(16))) char lds[KG * GBYTES > RED ? KG * GBYTES : RED];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int kg = wave / (WGM * 2), wrem = wave % (WGM * 2);
+    const int wm = wrem >> 1, wn = wrem & 1;
+    const int gt = tid - kg * NTG;   // thread index within the group
+    char* const halo = lds + kg * GBYTES;
+    char* const ring = halo + 2 * HPLANE;
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (a.xcd) {
         const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
@@ -373,19 +393,20 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
     const int y0 = (tl / tpr) * TR, x0 = (tl - (tl / tpr) * tpr) * TW;
     const int64_t mrow0 = (int64_t)bimg * HWo + (int64_t)y0 * W + x0;   // output pixel of tile position (0, 0)
 
-    const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR: a VGPR descriptor field costs a readfirstlane loop per load
+    // SGPR descriptor fields: a VGPR one costs a readfirstlane loop around every load
+    const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
 
-    // halo pieces of this thread: halo pixel (tid + it*NT) >> 3, channel quad tid & 7
-    const int kq = tid & 7;
+    // halo pieces of this thread: halo pixel (gt + it*NTG) >> 3, channel quad gt & 7
+    const int kq = gt & 7;
     int hpix[HIT];
 #pragma unroll
     for (int it = 0; it < HIT; ++it) {
-        const int hp = (tid + it * NT) >> 3;
+        const int hp = (gt + it * NTG) >> 3;
         int pix = -1;
         if (hp < NPX) {
             const int hr = hp / HW2, hc = hp - hr * HW2;
@@ -395,18 +416,21 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
         }
         hpix[it] = pix;
     }
-    // weight pieces: output channel row tid >> 2 (+ NT/4 per it), 16-B chunk tid & 3
-    const int bq = tid & 3;
+    // weight pieces: output channel row gt >> 2 (+ NTG/4 per it), 16-B chunk gt & 3
+    const int bq = gt & 3;
     unsigned bvoff[BIT];
 #pragma unroll
     for (int it = 0; it < BIT; ++it) {
-        const int n = n0 + (tid >> 2) + it * (NT / 4);
+        const int n = n0 + (gt >> 2) + it * (NTG / 4);
         bvoff[it] = n < a.Cout ? (unsigned)((n * a.K + 8 * bq) * 2) : 0x80000000u;
     }
 
+    // this workgroup's chunks [c0, c1); group kg takes c0 + KG*r + kg in round r
     const int nch = a.Ctot / 32;
     const int per = (nch + gridDim.z - 1) / gridDim.z;
     const int c0 = bz * per, c1 = min(nch, c0 + per);
+    const int nrounds = (max(c1 - c0, 0) + KG - 1) / KG;
+    auto chunk_of = [&](int r) { return c0 + KG * r + kg; };
 
     f4 rh[HIT];
     u4 wx_h[BIT], wx_l[BIT], wy_h[BIT], wy_l[BIT];   // weight slices two steps deep
@@ -415,8 +439,7 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
         const bool second = cb >= a.C1;
         const unsigned csrc4 = 4u * (second ? a.C2 : a.C1);
         const unsigned cofs4 = 4u * ((second ? cb - a.C1 : cb) + 4 * kq);
-        // one descriptor per branch: a selected descriptor lands in VGPRs and
-        // hipcc wraps every load in a readfirstlane loop
+        // one descriptor per branch (a selected descriptor would land in VGPRs)
         if (second) {
 #pragma unroll
             for (int it = 0; it < HIT; ++it) {
@@ -434,7 +457,7 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
     auto store_halo = [&]() {
 #pragma unroll
         for (int it = 0; it < HIT; ++it) {
-            const int e = tid + it * NT;
+            const int e = gt + it * NTG;
             if (e < NPX * 8) {
                 uint2 hv, lv;
                 split4_mix_x(rh[it], hv, lv);
@@ -444,9 +467,10 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
             }
         }
     };
-    // step s = (chunk c0 + s / 9, tap s % 9)
+    // step s = (round s / 9, tap s % 9)
     auto load_w = [&](int s, u4 (&rbh)[BIT], u4 (&rbl)[BIT]) {
-        const int c = c0 + s / 9, t = s % 9;
+        const int c = chunk_of(s / 9), t = s % 9;
+        if (c >= c1) return;
         const int soff = (t * a.Ctot + 32 * c) * 2;
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
@@ -458,7 +482,7 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
         char* base = ring + stage * BSTAGE;
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
-            const int off = xswz((tid >> 2) + it * (NT / 4), bq);
+            const int off = xswz((gt >> 2) + it * (NTG / 4), bq);
             *(u4*)(base + off) = rbh[it];
             *(u4*)(base + BPLANE + off) = rbl[it];
         }
@@ -480,46 +504,51 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
         hb[i] = (p / TW) * HW2 + (p % TW);
     }
     const int brow0 = wn * 64 + l32;
-    const int nsteps = (c1 - c0) * 9;
+    const int nsteps = nrounds * 9;
 
     // one step: prefetch the weights of step s + 2, MFMAs of step s on ring stage
-    // s & 1, then park step s + 1's weights (loaded a step ago) in the other stage
+    // s & 1, then park step s + 1's weights (loaded a step ago) in the other
+    // stage.  Every thread runs every step (the barriers are workgroup-wide); a
+    // group whose chunk of the round is past the range only skips its work.
     auto step = [&](int s, u4 (&ldh)[BIT], u4 (&ldl)[BIT], const u4 (&sth)[BIT], const u4 (&stl)[BIT]) {
-        const int c = c0 + s / 9, t = s % 9;
+        const int r = s / 9, t = s - 9 * r;
+        const int c = chunk_of(r);
         if (s + 2 < nsteps) load_w(s + 2, ldh, ldl);
-        if (t == 0 && c + 1 < c1) load_halo(c + 1);   // in registers until this chunk's taps are done
-        const int ty = t / 3;
-        const int tofs = ty * HW2 + (t - 3 * ty);
-        const char* wb = ring + (s & 1) * BSTAGE;
+        if (t == 0 && chunk_of(r + 1) < c1) load_halo(chunk_of(r + 1));   // in registers until this chunk's taps are done
+        if (c < c1) {
+            const int ty = t / 3;
+            const int tofs = ty * HW2 + (t - 3 * ty);
+            const char* wb = ring + (s & 1) * BSTAGE;
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            const int ch = 2 * s2 + hsel;
-            h8v fah[2], fal[2], fbh[2], fbl[2];
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int ch = 2 * s2 + hsel;
+                h8v fah[2], fal[2], fbh[2], fbl[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int off = xswz(hb[i] + tofs, ch);
-                fah[i] = *(const h8v*)(halo + off);
-                fal[i] = *(const h8v*)(halo + HPLANE + off);
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int off = xswz(brow0 + 32 * j, ch);
-                fbh[j] = *(const h8v*)(wb + off);
-                fbl[j] = *(const h8v*)(wb + BPLANE + off);
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i) {
+                    const int off = xswz(hb[i] + tofs, ch);
+                    fah[i] = *(const h8v*)(halo + off);
+                    fal[i] = *(const h8v*)(halo + HPLANE + off);
+                }
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                    const int off = xswz(brow0 + 32 * j, ch);
+                    fbh[j] = *(const h8v*)(wb + off);
+                    fbl[j] = *(const h8v*)(wb + BPLANE + off);
                 }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                    }
+            }
         }
-        if (s + 1 < nsteps) store_w((s + 1) & 1, sth, stl);
+        if (s + 1 < nsteps && chunk_of((s + 1) / 9) < c1) store_w((s + 1) & 1, sth, stl);
         __syncthreads();
-        if (t == 8 && s + 1 < nsteps) {   // every wave is past the last tap of chunk c
-            store_halo();
+        if (t == 8 && s + 1 < nsteps) {   // every wave is past the last tap of round r
+            if (chunk_of(r + 1) < c1) store_halo();
             __syncthreads();
         }
     };
@@ -527,13 +556,52 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_h_kernel(ConvArgs a) {
     if (nsteps > 0) {
         load_w(0, wx_h, wx_l);
         if (nsteps > 1) load_w(1, wy_h, wy_l);
-        load_halo(c0);
-        store_w(0, wx_h, wx_l);
-        store_halo();
+        if (chunk_of(0) < c1) {
+            load_halo(chunk_of(0));
+            store_w(0, wx_h, wx_l);
+            store_halo();
+        }
         __syncthreads();
         for (int s = 0; s < nsteps; s += 2) {
             step(s, wx_h, wx_l, wy_h, wy_l);
             if (s + 1 < nsteps) step(s + 1, wy_h, wy_l, wx_h, wx_l);
+        }
+    }
+
+    // combine the K groups through LDS: groups 1.. park their sums, group 0 adds
+    // them in group order (fixed summation order)
+    if constexpr (KG > 1) {
+        float* red = (float*)lds;   // (KG-1) x (WGM*2) waves x 64 floats x 64 lanes
+        constexpr int PER_WAVE = 4 * 16 * 64;
+        __syncthreads();            // the stages are free
+        if (kg > 0) {
+            float* dst = red + ((kg - 1) * WGM * 2 + wrem) * PER_WAVE;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; e += 4)
+                        *(f4*)(dst + ((i * 2 + j) * 16 + e) * 64 + 4 * lane) =
+                            f4{acc[i][j][e], acc[i][j][e + 1], acc[i][j][e + 2], acc[i][j][e + 3]};
+        }
+        __syncthreads();
+        if (kg > 0) return;
+#pragma unroll
+        for (int g = 1; g < KG; ++g) {
+            const float* src = red + ((g - 1) * WGM * 2 + wrem) * PER_WAVE;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; e += 4) {
+                        const f4 v = *(const f4*)(src + ((i * 2 + j) * 16 + e) * 64 + 4 * lane);
+                        acc[i][j][e] += v[0];
+                        acc[i][j][e + 1] += v[1];
+                        acc[i][j][e + 2] += v[2];
+                        acc[i][j][e + 3] += v[3];
+                    }
         }
     }
 
@@ -862,13 +930,21 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
     auto grid = [&](int bm, int bn) {
         return dim3((unsigned)ceil_div(a.M, bm), (unsigned)ceil_div(a.Cout, bn), splits);
     };
-    if (variant == 20) {   // K1h, 256-pixel blocks
+    if (variant == 20 || variant == 21) {   // K1h: 20 = 256-pixel blocks; 21 = 128-pixel blocks in 2 K groups
         const int tw = conv_h_tw(a);
-        CFD_REQUIRE(tw > 0, CFD_ESHAPE, "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");
-        const dim3 g = grid(256, 128);
-        if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
-        else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
+        CFD_REQUIRE(tw > 0 && (variant == 20 || (a.Hout * a.Wout) % 128 == 0), CFD_ESHAPE,
+                    "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");
+        if (variant == 20) {
+            const dim3 g = grid(256, 128);
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
+        } else {
+            const dim3 g = grid(128, 128);
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<128, 64, 2>), g, dim3(512), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<128, 32, 2>), g, dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<128, 16, 2>), g, dim3(512), 0, st, a);
+        }
         check_launch("conv_h_kernel");
         return splits;
     }
@@ -878,6 +954,10 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         case 2: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1>), grid(256, 128), dim3(512), 0, st, a); break;
         case 3: hipLaunchKernelGGL((conv_x_kernel<128, 64, 2, 1, 2>), grid(128, 64), dim3(256), 0, st, a); break;
         case 4: hipLaunchKernelGGL((conv_x_kernel<64, 128, 1, 2, 2>), grid(64, 128), dim3(256), 0, st, a); break;
+        case 5: hipLaunchKernelGGL((conv_x_kernel<64, 64, 1, 1, 4>), grid(64, 64), dim3(256), 0, st, a); break;
+        case 6: hipLaunchKernelGGL((conv_x_kernel<64, 64, 1, 1, 2>), grid(64, 64), dim3(128), 0, st, a); break;
+        case 7: hipLaunchKernelGGL((conv_x_kernel<128, 64, 2, 1, 1>), grid(128, 64), dim3(128), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((conv_x_kernel<64, 128, 1, 2, 1>), grid(64, 128), dim3(128), 0, st, a); break;
         case 10: hipLaunchKernelGGL((conv_y_kernel<4>), grid(128, 128), dim3(256), 0, st, a); break;
         case 11: hipLaunchKernelGGL((conv_y_kernel<3>), grid(128, 128), dim3(256), 0, st, a); break;
         case 12: hipLaunchKernelGGL((conv_y_kernel<4, 1>), grid(128, 128), dim3(256), 0, st, a); break;

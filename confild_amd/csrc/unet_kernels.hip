@@ -1368,12 +1368,13 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     if (kx && a.wbf && a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 &&
         srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31)) {
         ConvPlan q;
-        // K1h (halo tiles, conv_x.hip) where the image is at least 32x32: each
-        // activation fetched once per 32-channel chunk instead of once per tap
-        // (tools/convbench, same box: 1.19-1.29x K1x on the config-B 64^2/32^2
-        // shapes, 0.94x at 16^2); split-K over the chunks
+        // K1h (halo tiles, conv_x.hip) where a 256-pixel block tiles the image
+        // (16x16 and up): each activation fetched once per 32-channel chunk
+        // instead of once per tap (tools/convbench, same box: 1.19-1.29x K1x on
+        // the config-B 64^2/32^2 shapes, 1.04-1.17x at 16^2 with split-K 8);
+        // split-K over the chunks, at least one chunk per split
         static const int kh = env_int("CFD_CONV_KH", 1);
-        if (kh && (int64_t)a.Hout * a.Wout >= 1024 && conv_h_tw(a) > 0) {
+        if (kh && conv_h_tw(a) > 0) {
             q.kx = 20;
             q.bm = 256;
             q.bn = 128;
@@ -1381,7 +1382,7 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
             const int64_t t = ceil_div(mn, 256) * ceil_div(a.Cout, 128);
             const int nch = a.Ctot / 32;
             q.splits = 1;
-            while (t * q.splits < 256 && nch / (q.splits * 2) >= 2 && q.splits < 16) q.splits *= 2;
+            while (t * q.splits < 256 && q.splits * 2 <= nch && q.splits < 16) q.splits *= 2;
             while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
             return q;
         }

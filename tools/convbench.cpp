@@ -50,6 +50,14 @@ static const Shape SHAPES[] = {
     {"L2 conv 384->384", 8, 16, 16, 384, 0, 384, 3, 1, 0},
     {"L3 conv 512->512", 8, 8, 8, 512, 0, 512, 3, 1, 0},
     {"L0 skip1x1 384->128", 8, 64, 64, 256, 128, 128, 1, 1, 0},
+    {"L3 conv 1024->512", 8, 8, 8, 1024, 0, 512, 3, 1, 0},
+    {"L2 conv 768->384", 8, 16, 16, 768, 0, 384, 3, 1, 0},
+    {"L2 conv 896->384", 8, 16, 16, 896, 0, 384, 3, 1, 0},
+    {"L2 conv 640->384", 8, 16, 16, 640, 0, 384, 3, 1, 0},
+    {"L2 up 384->384", 8, 8, 8, 384, 0, 384, 3, 1, 1},
+    {"L3 qkv 512->1536", 8, 8, 8, 512, 0, 1536, 1, 1, 0},
+    {"L2 qkv 384->1152", 8, 16, 16, 384, 0, 1152, 1, 1, 0},
+    {"L1 qkv 256->768", 8, 32, 32, 256, 0, 768, 1, 1, 0},
     {"C4 384^2 conv 128->128", 1, 384, 384, 128, 0, 128, 3, 1, 0},
     {"C4 96^2 conv 256->256", 1, 96, 96, 256, 0, 256, 3, 1, 0},
     {"C4 48^2 conv 256->256", 1, 48, 48, 256, 0, 256, 3, 1, 0},
@@ -76,7 +84,9 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&st));
     std::mt19937 rng(7);
     std::uniform_real_distribution<float> U(-1.f, 1.f);
+    const char* filt = getenv("CX_SHAPES");   // only shapes whose name contains this
     for (const Shape& s : SHAPES) {
+        if (filt && !strstr(s.name, filt)) continue;
         const int Ctot = s.C1 + s.C2;
         const int Hout = s.up ? 2 * s.Hin : s.Hin / s.stride, Wout = s.up ? 2 * s.Win : s.Win / s.stride;
         const int M = s.B * Hout * Wout, K = s.ks * s.ks * Ctot;
@@ -166,16 +176,16 @@ int main(int argc, char** argv) {
         printf("%-26s M=%6d N=%4d K=%5d | K1s %3dx%3d/%d split %2d: %8.1f us %6.1f TF\n", s.name, M, s.Cout, K, p.bm,
                p.bn, p.nw, p.splits, ms0 * 1e3, flops / (ms0 * 1e-3) / 1e12);
         for (int v : variants) {
-            const int BMv_[] = {128, 128, 256, 128, 64}, BNv_[] = {128, 128, 128, 64, 128};
+            const int BMv_[] = {128, 128, 256, 128, 64, 64, 64, 128, 64}, BNv_[] = {128, 128, 128, 64, 128, 64, 64, 64, 128};
             const int vb = v >= 10 ? 0 : v;
-            const int BMv = v == 20 ? 256 : BMv_[vb], BNv = BNv_[vb];
+            const int BMv = v == 21 ? 128 : v >= 20 ? 256 : BMv_[vb], BNv = BNv_[vb];
             if (v >= 20 && !cfd::conv_h_tw(a)) continue;
             const int64_t tiles = ((M + BMv - 1) / BMv) * ((s.Cout + BNv - 1) / BNv);
             int splits = splits_x;
             if (!splits) {
                 splits = 1;
                 if (v >= 20)
-                    while (tiles * splits < 256 && Ctot / 32 / (splits * 2) >= 2 && splits < 16) splits *= 2;
+                    while (tiles * splits < 256 && Ctot / 32 / (splits * 2) >= (v == 21 ? 4 : 2) && splits < 16) splits *= 2;
                 else
                     while (tiles * splits < 256 && K / 32 / (splits * 2) >= 8 && splits < 16) splits *= 2;
             }
