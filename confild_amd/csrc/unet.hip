@@ -420,7 +420,11 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
 
     // GroupNorm(+SiLU) of `in` materialised once into nbuf (contiguous Ctot channels);
     // with a tape the scale/shift and group statistics are kept in *ss / *stats
-    auto gn = [&](const Act& in, const std::string& pre, int silu, float** ss, float** stats) -> Act {
+    // keep_raw == false: a deferred split-K sum this GroupNorm reduces is read by
+    // nothing else, so it is not stored (the GroupNorm of in_layers' output
+    // without a tape)
+    auto gn = [&](const Act& in, const std::string& pre, int silu, float** ss, float** stats,
+                  bool keep_raw = true) -> Act {
         cfd::GnArgs g{};
         g.src1 = in.a;
         g.src2 = in.b;
@@ -446,11 +450,15 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             g.kemb = pend.a.emb;
             g.kemb_stride = pend.a.emb_stride;
             g.kres = pend.a.res;
-            g.kx = pend.a.out;
+            g.kx = keep_raw ? pend.a.out : nullptr;
             pend.splits = 0;
         } else {
             flush();
         }
+        static const int gn_log = getenv("CFD_CONV_LOG") ? atoi(getenv("CFD_CONV_LOG")) : 0;
+        if (gn_log && launch)   // development: one line per GroupNorm, in launch order
+            fprintf(stderr, "GN %s %dx%d C=%d+%d ksplits=%d kres=%d kx=%d silu=%d\n", pre.c_str(), in.H, in.W, g.C1,
+                    g.C2, g.kpart ? g.ksplits : 0, g.kres ? 1 : 0, g.kx ? 1 : 0, silu);
         if (launch) cfd::launch_gn(g, B, st);
         return Act{nbuf, in.C(), nullptr, 0, in.H, in.W};
     };
@@ -574,7 +582,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, hb);
                 rec.h1 = hb;
                 const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
-                const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2);
+                const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2, /*keep_raw=*/tape != nullptr);
                 float* out = dest(cur.a, cur.b, nout);
                 conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};

@@ -295,7 +295,7 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
                     if (kres) y = rs[k][j] + y;
                     v[k][j] = y;
                 }
-                *(f4*)(kx + ib + k * istep) = v[k];
+                if (kx) *(f4*)(kx + ib + k * istep) = v[k];   // null: nobody reads the raw sum
             }
         }
     } else {

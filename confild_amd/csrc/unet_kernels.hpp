@@ -27,7 +27,7 @@ struct GnArgs {
     const float* kbias;
     const float* kemb;
     const float* kres;
-    float* kx;
+    float* kx;           // where the reduced sum is stored (null: nowhere, nobody reads it)
     int ksplits, kemb_stride;
 };
 
