@@ -1116,7 +1116,10 @@ __global__ __launch_bounds__(256) void attn_kv_split_kernel(AttnArgs a, int CH, 
     dst[stride] = lo;
 }
 
-template <int CH>
+// QT query tiles of 16 per wave: every K / V fragment a wave loads feeds QT x
+// the MFMAs (QT = 2 halves the fragment traffic per FLOP where T is long enough
+// to keep 256 workgroups of 64 QT queries).
+template <int CH, int QT = 1>
 __global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const h8v* __restrict__ kf,
                                                               const h8v* __restrict__ vf) {
     constexpr int NJ = CH / 32;  // 32-deep k-chunks of the head dimension
@@ -1126,7 +1129,7 @@ __global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const 
     const int h = blockIdx.y, heads = gridDim.y;
     const int64_t b = blockIdx.z;
     const int T = a.T, T32 = (T + 31) / 32 * 32;
-    const int q0 = blockIdx.x * 64 + wave * 16;
+    const int q0 = (blockIdx.x * 4 + wave) * 16 * QT;
     if (q0 >= T) return;  // wave-uniform
     const int C3 = 3 * a.C;
     const float* base = a.qkv + b * (int64_t)T * C3 + (int64_t)h * 3 * CH;
@@ -1134,88 +1137,107 @@ __global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const 
     const h8v* kfb = kf + bh * (T32 / 16) * NJ * 128 + lane;
     const h8v* vfb = vf + bh * (T32 / 32) * ND * 128 + lane;
 
-    h8v qh[NJ], ql[NJ];
-    {
-        const int tq = min(q0 + li, T - 1);
+    h8v qh[QT][NJ], ql[QT][NJ];
+#pragma unroll
+    for (int z = 0; z < QT; ++z) {
+        const int tq = min(q0 + 16 * z + li, T - 1);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const float* qp = base + (int64_t)tq * C3 + 32 * j + 8 * g;
             float v[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t) v[t] = qp[t] * a.scale;
-            split8_f16(v, qh[j], ql[j]);
+            split8_f16(v, qh[z][j], ql[z][j]);
         }
     }
-    f4 O[ND];
+    f4 O[QT][ND];
+    float mrun[QT], lrun[QT];
 #pragma unroll
-    for (int d = 0; d < ND; ++d) O[d] = f4{0.f, 0.f, 0.f, 0.f};
-    float mrun = -INFINITY, lrun = 0.f;
+    for (int z = 0; z < QT; ++z) {
+#pragma unroll
+        for (int d = 0; d < ND; ++d) O[z][d] = f4{0.f, 0.f, 0.f, 0.f};
+        mrun[z] = -INFINITY;
+        lrun[z] = 0.f;
+    }
 
     for (int kb = 0; kb < T32; kb += 32) {
         // S^T[key][query] of two 16-key tiles
-        f4 st[2];
+        f4 st[QT][2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            st[u] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int z = 0; z < QT; ++z) st[z][u] = f4{0.f, 0.f, 0.f, 0.f};
             const h8v* kp = kfb + (int64_t)((kb >> 4) + u) * NJ * 128;
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const h8v kh = kp[j * 128], kl = kp[j * 128 + 64];
-                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qh[j], st[u], 0, 0, 0);
-                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, ql[j], st[u], 0, 0, 0);
-                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[j], st[u], 0, 0, 0);
+#pragma unroll
+                for (int z = 0; z < QT; ++z) {
+                    st[z][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qh[z][j], st[z][u], 0, 0, 0);
+                    st[z][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, ql[z][j], st[z][u], 0, 0, 0);
+                    st[z][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[z][j], st[z][u], 0, 0, 0);
+                }
             }
         }
-        // lane (g, li) holds S[query li][key kb + 16u + 4g + r]
-        float mx = -INFINITY;
+        h8v ph[QT], pl[QT];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int z = 0; z < QT; ++z) {
+            // lane (g, li) holds S[query li][key kb + 16u + 4g + r]
+            float mx = -INFINITY;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                if (kb + 16 * u + 4 * g + r >= T) st[u][r] = -INFINITY;
-                mx = fmaxf(mx, st[u][r]);
-            }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mnew = fmaxf(mrun, mx);
-        const float alpha = expf(mrun - mnew);
-        float p[8], ps = 0.f;
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+                for (int r = 0; r < 4; ++r) {
+                    if (kb + 16 * u + 4 * g + r >= T) st[z][u][r] = -INFINITY;
+                    mx = fmaxf(mx, st[z][u][r]);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mnew = fmaxf(mrun[z], mx);
+            const float alpha = expf(mrun[z] - mnew);
+            float p[8], ps = 0.f;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                p[4 * u + r] = expf(st[u][r] - mnew);
-                ps += p[4 * u + r];
-            }
-        ps += __shfl_xor(ps, 16);
-        ps += __shfl_xor(ps, 32);
-        lrun = lrun * alpha + ps;
-        mrun = mnew;
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int d = 0; d < ND; ++d) O[d] = O[d] * alpha;
-        // O^T[d][query] += V^T[d][key] P^T[key][query]; element t of this lane's
-        // P^T operand is key kmap(g, t) = p[t]
-        h8v ph, pl;
-        split8_f16(p, ph, pl);
+                for (int r = 0; r < 4; ++r) {
+                    p[4 * u + r] = expf(st[z][u][r] - mnew);
+                    ps += p[4 * u + r];
+                }
+            ps += __shfl_xor(ps, 16);
+            ps += __shfl_xor(ps, 32);
+            lrun[z] = lrun[z] * alpha + ps;
+            mrun[z] = mnew;
+#pragma unroll
+            for (int d = 0; d < ND; ++d) O[z][d] = O[z][d] * alpha;
+            // element t of this lane's P^T operand is key kmap(g, t) = p[t]
+            split8_f16(p, ph[z], pl[z]);
+        }
+        // O^T[d][query] += V^T[d][key] P^T[key][query]
         const h8v* vp = vfb + (int64_t)(kb >> 5) * ND * 128;
 #pragma unroll
         for (int d = 0; d < ND; ++d) {
             const h8v vh = vp[d * 128], vl = vp[d * 128 + 64];
-            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, O[d], 0, 0, 0);
-            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, O[d], 0, 0, 0);
-            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, O[d], 0, 0, 0);
+#pragma unroll
+            for (int z = 0; z < QT; ++z) {
+                O[z][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph[z], O[z][d], 0, 0, 0);
+                O[z][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl[z], O[z][d], 0, 0, 0);
+                O[z][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph[z], O[z][d], 0, 0, 0);
+            }
         }
     }
     // lane (g, li) holds O[query li][16 d + 4 g + r]
-    const int tq = q0 + li;
-    if (a.lse && g == 0 && tq < T) a.lse[((int64_t)b * gridDim.y + h) * T + tq] = mrun + logf(lrun);
-    if (tq < T) {
-        float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
-        const float inv = 1.0f / lrun;
 #pragma unroll
-        for (int d = 0; d < ND; ++d) {
-            f4 v = O[d] * inv;
-            *(f4*)(op + 16 * d + 4 * g) = v;
+    for (int z = 0; z < QT; ++z) {
+        const int tq = q0 + 16 * z + li;
+        if (a.lse && g == 0 && tq < T) a.lse[((int64_t)b * gridDim.y + h) * T + tq] = mrun[z] + logf(lrun[z]);
+        if (tq < T) {
+            float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
+            const float inv = 1.0f / lrun[z];
+#pragma unroll
+            for (int d = 0; d < ND; ++d) {
+                f4 v = O[z][d] * inv;
+                *(f4*)(op + 16 * d + 4 * g) = v;
+            }
         }
     }
 }
@@ -1525,11 +1547,23 @@ void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* 
     hipLaunchKernelGGL(attn_kv_split_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, st, a, CH, heads, B,
                        kf, vf);
     check_launch("attn_kv_split_kernel");
-    const dim3 grid((unsigned)ceil_div(a.T, 64), heads, B);
-    switch (CH) {
-        case 32: hipLaunchKernelGGL(attention_split_kernel<32>, grid, dim3(256), 0, st, a, kf, vf); break;
-        case 64: hipLaunchKernelGGL(attention_split_kernel<64>, grid, dim3(256), 0, st, a, kf, vf); break;
-        case 128: hipLaunchKernelGGL(attention_split_kernel<128>, grid, dim3(256), 0, st, a, kf, vf); break;
+    // CFD_ATTN_QT=2: two query tiles per wave where that still leaves >= 256
+    // workgroups (per sample: the choice must not depend on the batch).  Measured
+    // slower (U-Net 4.48 -> 4.62 ms same-box: 181 registers halve the waves per
+    // SIMD, which costs more than the halved fragment traffic saves); off
+    static const int qt_env = env_int("CFD_ATTN_QT", 1);
+    const int qt = qt_env >= 2 && (int64_t)ceil_div(a.T, 128) * heads * 8 >= 256 ? 2 : 1;
+    const dim3 grid((unsigned)ceil_div(a.T, 64 * qt), heads, B);
+    if (qt == 1) switch (CH) {
+        case 32: hipLaunchKernelGGL((attention_split_kernel<32, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
+        case 64: hipLaunchKernelGGL((attention_split_kernel<64, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
+        case 128: hipLaunchKernelGGL((attention_split_kernel<128, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
+        default: throw Error{CFD_ESHAPE, "split attention head channels must be 32, 64 or 128"};
+    }
+    else switch (CH) {
+        case 32: hipLaunchKernelGGL((attention_split_kernel<32, 2>), grid, dim3(256), 0, st, a, kf, vf); break;
+        case 64: hipLaunchKernelGGL((attention_split_kernel<64, 2>), grid, dim3(256), 0, st, a, kf, vf); break;
+        case 128: hipLaunchKernelGGL((attention_split_kernel<128, 2>), grid, dim3(256), 0, st, a, kf, vf); break;
         default: throw Error{CFD_ESHAPE, "split attention head channels must be 32, 64 or 128"};
     }
     check_launch("attention_split_kernel");
