@@ -1262,21 +1262,53 @@ __global__ void temb_kernel(const int64_t* __restrict__ t, const float* __restri
 }
 
 // y[b][n] = bias[n] + sum_k W[n][k] * act(x[b][k]); one wave per output feature.
-__global__ void linear_kernel(const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-                              float* __restrict__ y, int B, int K, int N, int act) {
+// y[b][n] = W[n] . act(x[b]) + bias[n] (time_embed, emb_layers): a bandwidth
+// problem (the weights are read once, ~15 MB for all emb_layers at config B).
+// One wave per output feature, its weight row held in registers as KW float4s
+// per lane (K <= 256 KW); act(x) staged once per workgroup in LDS, 8 samples at
+// a time; fixed-order lane reduction per sample (batch-invariant: sample b's
+// sum does not depend on B).
+template <int KW>
+__global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                     const float* __restrict__ bias, float* __restrict__ y, int B,
+                                                     int K, int N, int act) {
+    constexpr int BC = 8;   // samples per LDS chunk
+    extern __shared__ __attribute__((aligned(16))) float xs[];   // BC x K
     const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (n >= N) return;
-    const float* wr = W + (int64_t)n * K;
-    for (int b = 0; b < B; ++b) {
-        const float* xb = x + (int64_t)b * K;
-        float s = 0.f;
-        for (int k = lane; k < K; k += 64) {
-            const float v = act ? silu_f(xb[k]) : xb[k];
-            s = fmaf(wr[k], v, s);
+    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const bool live = n < N;
+    f4 w[KW];
+#pragma unroll
+    for (int i = 0; i < KW; ++i) {
+        const int k = 4 * (lane + 64 * i);
+        w[i] = live && k < K ? *(const f4*)(W + (int64_t)n * K + k) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float bn = live ? bias[n] : 0.f;
+    for (int b0 = 0; b0 < B; b0 += BC) {
+        const int nb = min(BC, B - b0);
+        __syncthreads();   // the previous chunk's readers are done
+        for (int i = threadIdx.x; i < nb * K; i += 256) {
+            const float v = x[(int64_t)b0 * K + i];
+            xs[i] = act ? silu_f(v) : v;
         }
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        if (lane == 0) y[(int64_t)b * N + n] = s + bias[n];
+        __syncthreads();
+        if (!live) continue;
+        for (int bb = 0; bb < nb; ++bb) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < KW; ++i) {
+                const int k = 4 * (lane + 64 * i);
+                if (k < K) {
+                    const f4 v = *(const f4*)(xs + bb * K + k);
+                    s = fmaf(w[i][0], v[0], s);
+                    s = fmaf(w[i][1], v[1], s);
+                    s = fmaf(w[i][2], v[2], s);
+                    s = fmaf(w[i][3], v[3], s);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            if (lane == 0) y[(int64_t)(b0 + bb) * N + n] = s + bn;
+        }
     }
 }
 
@@ -1576,7 +1608,13 @@ void launch_temb(const int64_t* t, const float* freqs, float* out, int dim, int 
 
 void launch_linear(const float* x, const float* W, const float* bias, float* y, int B, int K, int N, int act,
                    hipStream_t st) {
-    hipLaunchKernelGGL(linear_kernel, dim3((unsigned)ceil_div(N, 4)), dim3(256), 0, st, x, W, bias, y, B, K, N, act);
+    CFD_REQUIRE(K % 4 == 0 && K <= 2048, CFD_ESHAPE, "linear: K must be a multiple of 4, at most 2048");
+    const dim3 g((unsigned)ceil_div(N, 4));
+    const size_t lds = sizeof(float) * 8 * K;
+    if (K <= 256) hipLaunchKernelGGL(linear_kernel<1>, g, dim3(256), lds, st, x, W, bias, y, B, K, N, act);
+    else if (K <= 512) hipLaunchKernelGGL(linear_kernel<2>, g, dim3(256), lds, st, x, W, bias, y, B, K, N, act);
+    else if (K <= 1024) hipLaunchKernelGGL(linear_kernel<4>, g, dim3(256), lds, st, x, W, bias, y, B, K, N, act);
+    else hipLaunchKernelGGL(linear_kernel<8>, g, dim3(256), lds, st, x, W, bias, y, B, K, N, act);
     check_launch("linear_kernel");
 }
 
