@@ -24,7 +24,8 @@ struct UParam {
     size_t count = 0;
     int emb_row = 0;     // EmbW/EmbB: first row in the concatenated emb matrix
     bool set = false;
-    int tpack = 0;       // input-gradient pack: 0 none, 1 transposed (Cin, taps, Cout), 2 upsample 4x4 (Cin, 16, Cout)
+    int tpack = 0;       // input-gradient pack: 0 none, 1 transposed (Cin, taps, Cout), 2 upsample 4x4 (Cin, 16, Cout),
+                         // 3 transposed with mirrored taps (a stride-1 3x3 input-gradient as a plain convolution)
     size_t toffset = 0;  // floats into the transposed arena
     float split_inv = 1.f;  // split compute: 1 / s, s = power-of-two scale of this conv weight
     float tsplit_inv = 1.f; // the same for the input-gradient pack
@@ -91,12 +92,13 @@ void add_param(cfd_unet* h, const std::string& key, std::vector<int64_t> shape, 
     h->params.push_back(p);
 }
 
-void add_conv(cfd_unet* h, const std::string& pre, int cin, int cout, int k, bool conv1d = false, bool up = false) {
+void add_conv(cfd_unet* h, const std::string& pre, int cin, int cout, int k, bool conv1d = false, bool up = false,
+              bool mirror = false) {
     if (conv1d)
         add_param(h, pre + ".weight", {cout, cin, 1}, Pack::Conv1);
     else
         add_param(h, pre + ".weight", {cout, cin, k, k}, k == 3 ? Pack::Conv3 : Pack::Conv1);
-    h->params.back().tpack = up ? 2 : 1;
+    h->params.back().tpack = up ? 2 : mirror ? 3 : 1;
     add_param(h, pre + ".bias", {cout}, Pack::Raw);
 }
 
@@ -107,11 +109,11 @@ void add_norm(cfd_unet* h, const std::string& pre, int c) {
 
 int add_res(cfd_unet* h, const std::string& pre, int cin, int cout) {
     add_norm(h, pre + ".in_layers.0", cin);
-    add_conv(h, pre + ".in_layers.2", cin, cout, 3);
+    add_conv(h, pre + ".in_layers.2", cin, cout, 3, false, false, /*mirror=*/true);
     add_param(h, pre + ".emb_layers.1.weight", {cout, h->tdim}, Pack::EmbW, h->emb_total);
     add_param(h, pre + ".emb_layers.1.bias", {cout}, Pack::EmbB, h->emb_total);
     add_norm(h, pre + ".out_layers.0", cout);
-    add_conv(h, pre + ".out_layers.3", cout, cout, 3);
+    add_conv(h, pre + ".out_layers.3", cout, cout, 3, false, false, /*mirror=*/true);
     if (cin != cout) add_conv(h, pre + ".skip_connection", cin, cout, 1);
     h->res.push_back({pre, cin, cout, h->emb_total});
     h->emb_total += cout;
@@ -776,12 +778,13 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 const auto& rs = h->res[s.idx];
                 const float* dout = dcur.a;
                 float* G = gfree(dout);
-                dconv(dout, rs.cout, in.H, in.W, rs.pre + ".out_layers.3.weight", rs.cout, in.H, in.W, 3, 1, 1, 1, G);
+                // stride-1 3x3: plain convolutions with the mirrored packs (tpack 3)
+                dconv(dout, rs.cout, in.H, in.W, rs.pre + ".out_layers.3.weight", rs.cout, in.H, in.W, 3, 1, 1, 0, G);
                 float* dh1 = gfree(dout, G);
                 gnb(Act{r.h1, rs.cout, nullptr, 0, in.H, in.W}, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr,
                     dh1, nullptr);
                 // G <- in_layers conv input-gradient (Ctot channels)
-                dconv(dh1, rs.cout, in.H, in.W, rs.pre + ".in_layers.2.weight", in.C(), in.H, in.W, 3, 1, 1, 1, G);
+                dconv(dh1, rs.cout, in.H, in.W, rs.pre + ".in_layers.2.weight", in.C(), in.H, in.W, 3, 1, 1, 0, G);
                 const float* addsrc = dout;
                 if (rs.cin != rs.cout) {
                     float* sk = gfree(dout, G, dh1);
@@ -965,18 +968,22 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
         }
         if (p.tpack) {
             // input-gradient packs.  1: W^T as (Cin, tap, Cout) (taps not mirrored:
-            // conv_gemm's TMODE gathers dY[(o + pad - tap) / stride]).  2: Upsample +
+            // conv_gemm's TMODE gathers dY[(o + pad - tap) / stride]).  3: the same
+            // with tap t stored at taps-1-t: for a stride-1 3x3 pad-1 convolution
+            // dX[o] = sum_t W_t^T dY[o + 1 - t] is a plain convolution of dY with the
+            // mirrored taps, so it runs on the forward kernels (K1h).  2: Upsample +
             // conv3x3 as a 4x4 stride-2 pad-1 convolution of dY: per axis, tap e of
             // the 4 sums the 3x3 taps d with a - d + 2 == e over the two nearest
             // neighbours a in {0, 1}:  e0 = w2, e1 = w1 + w2, e2 = w0 + w1, e3 = w0.
             const int64_t co = p.shape[0], ci = p.shape[1];
             const int taps = (int)(p.count / (size_t)(co * ci));
             std::vector<float> pk(p.tpack == 2 ? (size_t)ci * 16 * co : n);
-            if (p.tpack == 1) {
+            if (p.tpack == 1 || p.tpack == 3) {
                 for (int64_t o = 0; o < co; ++o)
                     for (int64_t i = 0; i < ci; ++i)
                         for (int tap = 0; tap < taps; ++tap)
-                            pk[((size_t)i * taps + tap) * co + o] = host[((size_t)o * ci + i) * taps + tap];
+                            pk[((size_t)i * taps + (p.tpack == 3 ? taps - 1 - tap : tap)) * co + o] =
+                                host[((size_t)o * ci + i) * taps + tap];
             } else {
                 static const int dlo[4] = {2, 1, 0, 0}, dhi[4] = {2, 2, 1, 0};
                 for (int64_t o = 0; o < co; ++o)
