@@ -8,6 +8,23 @@
 
 #include "../../include/confild.h"
 
+// Device-side index assertions of the bounds-checked build (make DEBUG=1 ->
+// lib/libconfild_hip_debug.so, selected with CFD_LIB=libconfild_hip_debug.so):
+// a failing check prints its site and traps the wave (the launch fails, the
+// process sees a HIP error).  Compiled out of the shipped library.
+#ifdef CFD_DEBUG
+#define CFD_DASSERT(cond)                                                                         \
+    do {                                                                                          \
+        if (!(cond)) {                                                                            \
+            printf("CFD_DASSERT failed %s:%d: %s (block %d,%d,%d thread %d)\n", __FILE__, __LINE__, #cond, \
+                   (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)threadIdx.x);         \
+            __builtin_trap();                                                                     \
+        }                                                                                         \
+    } while (0)
+#else
+#define CFD_DASSERT(cond) ((void)0)
+#endif
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

@@ -45,7 +45,10 @@ __device__ __forceinline__ void split4_mix_x(const f4& x, uint2& hi, uint2& lo) 
     asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.y) : "v"(x[3]), "v"(hi.y));
 }
 
-template <int BM, int BN, int WGM, int WGN, int KG>
+// PF: tiles in flight through registers (1: the next tile; 2: two ahead, two
+// register sets -- for short per-workgroup K ranges where one tile of compute
+// does not cover a load's latency).
+template <int BM, int BN, int WGM, int WGN, int KG, int PF = 1>
 __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs a) {
     constexpr int NW = WGM * WGN * KG, NT = 64 * NW;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
@@ -63,16 +66,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     const int kg = wave / (WGM * WGN), wrem = wave % (WGM * WGN);
     const int wm = wrem / WGN, wn = wrem % WGN;
 
-    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (a.xcd) {   // XCD-contiguous tile order, splits fastest (as conv_gemm_kernel)
-        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
-        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
-        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
-        bz = Lp % gz;
-        by = (Lp / gz) % gy;
-        bx = Lp / (gz * gy);
-    }
+    int bx, by, bz;
+    xcd_tile(a.xcd, bx, by, bz);
     const int m0 = bx * BM, n0 = by * BN;
     const int HWo = a.Hout * a.Wout;
     const int kq = tid & 7, rsub = tid >> 3;
@@ -110,6 +105,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
                 }
                 if (ok) pix = (b * a.Hin + iy) * a.Win + ix;
             }
+            CFD_DASSERT(pix < srows);
             pixtab[e] = pix;
         }
     }
@@ -148,9 +144,9 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     }
     __syncthreads();   // pixtab
 
-    f4 ra[AIT];
-    uint2 rbh[BIT], rbl[BIT];
-    auto load_tile = [&](int kt) {   // tiles kt + g, g < KG
+    f4 ra[PF][AIT];
+    uint2 rbh[PF][BIT], rbl[PF][BIT];
+    auto load_tile = [&](int kt, int set) {   // tiles kt + g, g < KG, into register set `set`
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             const int g = a_g[it];
@@ -160,15 +156,15 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
             const unsigned cofs4 = 4u * ((second ? cb - a.C1 : cb) + 4 * kq);
             const int pix = kt + g < kt1 ? pixtab[tpg[g] * BM + a_m[it]] : -1;
             const unsigned off = pix >= 0 ? __umul24((unsigned)pix, csrc4) + cofs4 : 0x80000000u;
-            ra[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(second ? rs2 : rs1, off, 0, 0));
+            ra[set][it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(second ? rs2 : rs1, off, 0, 0));
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
             const int g = b_g[it];
             const unsigned voff = kt + g < kt1 ? b_voff[it] : 0x80000000u;
             const int soff = (tpg[g] * a.Ctot + cbg[g]) * 2;
-            rbh[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, voff, soff, 0));
-            rbl[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, voff, soff, 0));
+            rbh[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, voff, soff, 0));
+            rbl[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, voff, soff, 0));
         }
 #pragma unroll
         for (int g = 0; g < KG; ++g) {
@@ -179,12 +175,12 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
             }
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf, int set) {
         char* base = lds + buf * STAGE;
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             uint2 hv, lv;
-            split4_mix_x(ra[it], hv, lv);
+            split4_mix_x(ra[set][it], hv, lv);
             const int off = xswz(a_row[it], kq >> 1) + (kq & 1) * 8;
             *(uint2*)(base + off) = hv;
             *(uint2*)(base + ABYTES + off) = lv;
@@ -192,8 +188,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
             const int off = xswz(b_row[it], kq >> 1) + (kq & 1) * 8;
-            *(uint2*)(base + 2 * ABYTES + off) = rbh[it];
-            *(uint2*)(base + 2 * ABYTES + BBYTES + off) = rbl[it];
+            *(uint2*)(base + 2 * ABYTES + off) = rbh[set][it];
+            *(uint2*)(base + 2 * ABYTES + BBYTES + off) = rbl[set][it];
         }
     };
 
@@ -207,14 +203,12 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 
     const int l32 = lane & 31, hsel = lane >> 5;
     const int arow0 = kg * BM + wm * WTM + l32, brow0 = kg * BN + wn * WTN + l32;
-    if (kt0 < kt1) {
-        load_tile(kt0);
-        store_tile(0);
-        __syncthreads();
-        int cur = 0;
-        for (int kt = kt0; kt < kt1; kt += KG) {
+    // one K step (tiles kt + g): prefetch the tiles PF steps ahead into register
+    // set `lset`, MFMAs on LDS stage `cur`, then stage the next step's tiles
+    // (register set `sset`, loaded PF - 1 steps ago) into the other LDS stage
+    auto kstep = [&](int kt, int cur, int lset, int sset) {
             const bool more = kt + KG < kt1;
-            if (more) load_tile(kt + KG);
+            if (kt + PF * KG < kt1) load_tile(kt + PF * KG, lset);
             const char* base = lds + cur * STAGE;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -241,9 +235,27 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
                     }
             }
-            if (more) store_tile(cur ^ 1);
+            if (more) store_tile(cur ^ 1, sset);
             __syncthreads();
-            cur ^= 1;
+    };
+    if (kt0 < kt1) {
+        load_tile(kt0, 0);
+        if constexpr (PF == 2) {
+            if (kt0 + KG < kt1) load_tile(kt0 + KG, 1);
+        }
+        store_tile(0, 0);
+        __syncthreads();
+        if constexpr (PF == 1) {
+            int cur = 0;
+            for (int kt = kt0; kt < kt1; kt += KG) {
+                kstep(kt, cur, 0, 0);
+                cur ^= 1;
+            }
+        } else {
+            for (int kt = kt0; kt < kt1; kt += 2 * KG) {
+                kstep(kt, 0, 0, 1);
+                if (kt + KG < kt1) kstep(kt + KG, 1, 1, 0);
+            }
         }
     }
 
@@ -357,7 +369,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // clock the chip holds under it, ~0.52 of the 2.4 GHz split-f16 peak.
 template <int BM, int TW, int KG = 1>
 __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
-    constexpr int BN = 128, WGM = BM / 64, NTG = 64 * WGM * 2, NT = NTG * KG;   // threads per group / total
+    constexpr int BN = 128, WGM = BM / 64, NTG = 64 * WGM * 2;   // threads per K group (the workgroup: NTG * KG)
     constexpr int TR = BM / TW, HW2 = TW + 2, NPX = (TR + 2) * HW2;
     constexpr int HPLANE = NPX * 64;                  // one f16 plane of the halo (64 B per pixel)
     constexpr int HIT = (NPX * 8 + NTG - 1) / NTG;    // 16-B halo pieces per thread
@@ -375,16 +387,8 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     const int gt = tid - kg * NTG;   // thread index within the group
     char* const halo = lds + kg * GBYTES;
     char* const ring = halo + 2 * HPLANE;
-    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (a.xcd) {
-        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
-        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
-        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
-        bz = Lp % gz;
-        by = (Lp / gz) % gy;
-        bx = Lp / (gz * gy);
-    }
+    int bx, by, bz;
+    xcd_tile(a.xcd, bx, by, bz);
     const int n0 = by * BN;
     const int W = a.Wout, HWo = a.Hout * W;
     // tile bx -> sample, block row, block column (row-major blocks in a sample)
@@ -392,6 +396,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     const int bimg = bx / tps, tl = bx - bimg * tps;
     const int y0 = (tl / tpr) * TR, x0 = (tl - (tl / tpr) * tpr) * TW;
     const int64_t mrow0 = (int64_t)bimg * HWo + (int64_t)y0 * W + x0;   // output pixel of tile position (0, 0)
+    CFD_DASSERT(mrow0 + (int64_t)(TR - 1) * W + TW <= a.M && HWo % BM == 0 && W % TW == 0);
 
     // SGPR descriptor fields: a VGPR one costs a readfirstlane loop around every load
     const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));
@@ -414,6 +419,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
             if (iy >= 0 && iy < a.Hout && ix >= 0 && ix < W)
                 pix = a.up ? (bimg * a.Hin + (iy >> 1)) * a.Win + (ix >> 1) : (bimg * a.Hin + iy) * a.Win + ix;
         }
+        CFD_DASSERT(pix < srows);
         hpix[it] = pix;
     }
     // weight pieces: output channel row gt >> 2 (+ NTG/4 per it), 16-B chunk gt & 3
@@ -525,6 +531,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
                 h8v fah[2], fal[2], fbh[2], fbl[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
+                    CFD_DASSERT(hb[i] + tofs < NPX);
                     const int off = xswz(hb[i] + tofs, ch);
                     fah[i] = *(const h8v*)(halo + off);
                     fal[i] = *(const h8v*)(halo + HPLANE + off);
@@ -693,16 +700,8 @@ __global__ __launch_bounds__(256, 1) void conv_y_kernel(ConvArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave >> 1, wn = wave & 1;
-    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (a.xcd) {
-        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
-        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
-        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
-        bz = Lp % gz;
-        by = (Lp / gz) % gy;
-        bx = Lp / (gz * gy);
-    }
+    int bx, by, bz;
+    xcd_tile(a.xcd, bx, by, bz);
     const int m0 = bx * BM, n0 = by * BN;
     const int HWo = a.Hout * a.Wout;
 
@@ -958,6 +957,8 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         case 6: hipLaunchKernelGGL((conv_x_kernel<64, 64, 1, 1, 2>), grid(64, 64), dim3(128), 0, st, a); break;
         case 7: hipLaunchKernelGGL((conv_x_kernel<128, 64, 2, 1, 1>), grid(128, 64), dim3(128), 0, st, a); break;
         case 8: hipLaunchKernelGGL((conv_x_kernel<64, 128, 1, 2, 1>), grid(64, 128), dim3(128), 0, st, a); break;
+        case 9: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1, 2>), grid(128, 128), dim3(256), 0, st, a); break;
+        case 23: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1, 2>), grid(256, 128), dim3(512), 0, st, a); break;
         case 10: hipLaunchKernelGGL((conv_y_kernel<4>), grid(128, 128), dim3(256), 0, st, a); break;
         case 11: hipLaunchKernelGGL((conv_y_kernel<3>), grid(128, 128), dim3(256), 0, st, a); break;
         case 12: hipLaunchKernelGGL((conv_y_kernel<4, 1>), grid(128, 128), dim3(256), 0, st, a); break;

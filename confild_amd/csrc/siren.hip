@@ -855,7 +855,7 @@ extern "C" int cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, c
         size_t need = 0;
         cfd_siren_workspace_bytes(h, b, &need);
         CFD_REQUIRE(ws && ws_bytes >= need, CFD_EARG, "workspace too small");
-        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features, L = h->cfg.in_latent_features;
+        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features;
         auto st = (hipStream_t)stream;
         float* film = (float*)ws;
         film_vectors(h, latents, b, film, st);
@@ -999,7 +999,6 @@ extern "C" int cfd_siren_tape_forward(cfd_siren* h, const float* coords, int64_t
         size_t need = 0;
         cfd_siren_vjp_workspace_bytes(h, Ns, R, &need);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features, L = h->cfg.in_latent_features;
         auto st = (hipStream_t)stream;
         cfd::SirenTapeArgs a{};
         tape_args(h, a, Ns, R, ws);

@@ -469,6 +469,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
     const int h = lane >> 5;
     const int64_t b = p.b0 + blockIdx.y;
     const int64_t n = (int64_t)blockIdx.x * TILE + wave * 32 + (lane & 31);
+    CFD_DASSERT(p.d >= 1 && p.d <= 4 && p.c >= 1 && p.c <= 4 && nh >= 1);
 
     {
         const float* fsrc = p.film + b * (int64_t)(nh + 1) * H;

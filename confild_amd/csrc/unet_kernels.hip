@@ -239,6 +239,7 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     const int Ctot = a.Ctot, cpg = Ctot / 32, nq = cpg / 4;
     const int HW = a.HW;
     const int rows = NT / nq;
+    CFD_DASSERT(grp < 32 && nq >= 1 && (HW + rows - 1) / rows <= IPT);   // every pixel has a register slot
     const int t = threadIdx.x;
     const bool act = t < rows * nq;
     const int q = t % nq, r0 = t / nq;
@@ -444,16 +445,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     // dispatch); hand XCD x the x-th contiguous run of the (m, n, split) tiles,
     // splits fastest, so the workgroups sharing an XCD's L2 share activation rows
     // (the 3x3 halo and every split of one pixel tile) instead of striding the image.
-    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (a.xcd) {
-        const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
-        const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-        const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
-        const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
-        bz = Lp % gz;
-        by = (Lp / gz) % gy;
-        bx = Lp / (gz * gy);
-    }
+    int bx, by, bz;
+    xcd_tile(a.xcd, bx, by, bz);
     const int m0 = bx * BM, n0 = by * BN;
     const int HWo = a.Hout * a.Wout;
     const int kq = tid & 7, rsub = tid >> 3;  // 8 threads per 32-float row
@@ -573,6 +566,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                 }
                 if (ok) pix = (b * a.Hin + iy) * a.Win + ix;
             }
+            CFD_DASSERT(pix < srows);
             pixtab[e] = pix;
         }
         __syncthreads();
@@ -1131,6 +1125,7 @@ __global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const 
     const int T = a.T, T32 = (T + 31) / 32 * 32;
     const int q0 = (blockIdx.x * 4 + wave) * 16 * QT;
     if (q0 >= T) return;  // wave-uniform
+    CFD_DASSERT(h * CH + CH <= a.C);
     const int C3 = 3 * a.C;
     const float* base = a.qkv + b * (int64_t)T * C3 + (int64_t)h * 3 * CH;
     const int64_t bh = b * heads + h;
@@ -1277,6 +1272,7 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ x
     const int lane = threadIdx.x & 63;
     const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool live = n < N;
+    CFD_DASSERT(K <= 256 * KW && K % 4 == 0);
     f4 w[KW];
 #pragma unroll
     for (int i = 0; i < KW; ++i) {
@@ -1499,7 +1495,9 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     static const int korder = env_int("CFD_CONV_KORDER", 0);
     static const int bufaddr = env_int("CFD_CONV_BUFADDR", 1);
     ConvArgs b = a;
-    b.xcd = xcd ? 1 : 0;
+    // 1: splits-fastest XCD order; 2: m-fastest (weight-sharing) order; 3: order 2 where
+    // the per-sample image has <= 256 pixels (the small-M levels), else 1
+    b.xcd = xcd == 3 ? ((int64_t)a.Hout * a.Wout <= 256 ? 2 : 1) : xcd < 0 || xcd > 2 ? 1 : xcd;
     b.korder = korder ? 1 : 0;
     {   // 32-bit buffer offsets and 24-bit pixel indices must hold
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));

@@ -117,6 +117,31 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer
 void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st);
 // K1x (conv_x.hip): split-f16 forward convolution on 32x32x16 MFMAs with 64x64
 // wave tiles and an in-workgroup K split; variant selects the tile shape
+// Workgroup -> (m tile, n tile, split) in XCD-contiguous order (the hardware
+// deals workgroups round-robin over the 8 XCDs): XCD x gets the x-th contiguous
+// run of tiles.  order 1: splits fastest, then n, then m (the workgroups of an
+// XCD share activation rows: every split of one pixel tile); order 2: m fastest,
+// then splits, then n (they share weight slices: the small-M levels, where a
+// weight slice is read by every m tile).
+__device__ __forceinline__ void xcd_tile(int order, int& bx, int& by, int& bz) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    bz = blockIdx.z;
+    if (!order) return;
+    const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+    const unsigned T = gx * gy * gz, L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const unsigned q = T >> 3, r = T & 7, x = L & 7, sl = L >> 3;
+    const unsigned Lp = x < r ? x * (q + 1) + sl : r * (q + 1) + (x - r) * q + sl;
+    if (order == 2) {
+        bx = Lp % gx;
+        bz = (Lp / gx) % gz;
+        by = Lp / (gx * gz);
+    } else {
+        bz = Lp % gz;
+        by = (Lp / gz) % gy;
+        bx = Lp / (gz * gy);
+    }
+}
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st);
 int conv_h_tw(const ConvArgs& a);   // K1h tile width for a shape, 0: not applicable
 void launch_conv_in(const ConvArgs& a, hipStream_t st);

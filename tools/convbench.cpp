@@ -176,15 +176,15 @@ int main(int argc, char** argv) {
         printf("%-26s M=%6d N=%4d K=%5d | K1s %3dx%3d/%d split %2d: %8.1f us %6.1f TF\n", s.name, M, s.Cout, K, p.bm,
                p.bn, p.nw, p.splits, ms0 * 1e3, flops / (ms0 * 1e-3) / 1e12);
         for (int v : variants) {
-            const int BMv_[] = {128, 128, 256, 128, 64, 64, 64, 128, 64}, BNv_[] = {128, 128, 128, 64, 128, 64, 64, 64, 128};
+            const int BMv_[] = {128, 128, 256, 128, 64, 64, 64, 128, 64, 128}, BNv_[] = {128, 128, 128, 64, 128, 64, 64, 64, 128, 128};
             const int vb = v >= 10 ? 0 : v;
             const int BMv = v == 21 ? 128 : v >= 20 ? 256 : BMv_[vb], BNv = BNv_[vb];
-            if (v >= 20 && !cfd::conv_h_tw(a)) continue;
+            if ((v == 20 || v == 21) && !cfd::conv_h_tw(a)) continue;
             const int64_t tiles = ((M + BMv - 1) / BMv) * ((s.Cout + BNv - 1) / BNv);
             int splits = splits_x;
             if (!splits) {
                 splits = 1;
-                if (v >= 20)
+                if (v == 20 || v == 21)
                     while (tiles * splits < 256 && Ctot / 32 / (splits * 2) >= (v == 21 ? 4 : 2) && splits < 16) splits *= 2;
                 else
                     while (tiles * splits < 256 && K / 32 / (splits * 2) >= 8 && splits < 16) splits *= 2;
