@@ -55,6 +55,11 @@ C_COORDS = 1 << 22
 C_LATENTS = 256
 FMA_PEAK_TFLOPS = 157.3    # MI355X fp32 matrix peak (MI355X_MICROARCH.md chip table)
 F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16/bf16 matrix peak (same table; no sparsity)
+# measured: every SIMD issuing v_mfma_f32_32x32x16_f16 back to back on random
+# operands holds ~1.62 GHz, 1693.5 TFLOP/s f16 (zero operands: 2477 at 2.36 GHz);
+# tools/mfma_peak.cpp, profiles/r02_mfma_peak.json.  /3 = the ceiling a split-f16
+# kernel can reach on real data at the clock the chip holds
+F16_SUSTAINED_TFLOPS = 1693.5
 UNET_FLOPS_PER_SAMPLE = 68.61e9   # config-B U-Net forward, 2*MAC of conv/bmm/addmm (FlopCounter)
 METRIC = "generated fields/sec (256-step sample + CNF decode), Case4 latent, 1/2/4/8 GPU"
 
@@ -505,8 +510,9 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": args.scaling if args.config == "B" else "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded weights and inputs; no checkpoints)",
-            "compute": {"unet": ("fp32 via split-f16 convolutions (3x v_mfma_f32_16x16x32_f16 on 22-bit operand "
-                                 "splits; error vs fp64 = fp32's, DESIGN.md K1s); GroupNorm/softmax/attention fp32"
+            "compute": {"unet": ("fp32 via split-f16 convolutions (3x v_mfma_f32_32x32x16/16x16x32_f16 on 22-bit "
+                                 "operand splits; error vs fp64 = fp32's, DESIGN.md K1h/K1x/K1s); "
+                                 "GroupNorm/softmax fp32, attention split-f16 (K4s)"
                                  if args.config == "B" and o["model"].compute == "split_f16" else
                                  "fp32 (v_mfma_f32_16x16x4_f32)" if args.config == "B" else None),
                         "cnf_decoder": ("fp32 via split-f16 (3x v_mfma_f32_32x32x16_f16 on 22-bit operand "
@@ -517,7 +523,12 @@ def main():
             "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)", "achieved": achieved,
                          "peak": peak, "peak_basis": peak_basis, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": measured_traffic(mode, rows_local, npts) if args.config == "B" else None,
-                         "flops_per_launch": flops, "launch_ms": dec_ms, "pmc": measured_mfma_util(kname)},
+                         "flops_per_launch": flops, "launch_ms": dec_ms, "pmc": measured_mfma_util(kname),
+                         **({"peak_sustained": F16_SUSTAINED_TFLOPS / 3,
+                             "frac_sustained": achieved / (F16_SUSTAINED_TFLOPS / 3),
+                             "sustained_basis": "measured back-to-back f16 MFMA on random operands / 3 "
+                                                "(tools/mfma_peak.cpp, profiles/r02_mfma_peak.json)"}
+                            if mode == "split_f16" else {})},
             "cpu_baseline": cpu,
         }
         if args.config == "B":
@@ -527,7 +538,9 @@ def main():
                                     "achieved": ua, "peak": F16_PEAK_TFLOPS / 3,
                                     "peak_basis": "f16 dense MFMA peak / 3 (split-f16 convolutions)",
                                     "unit": "TFLOP/s", "frac": ua / (F16_PEAK_TFLOPS / 3), "flops": uf,
-                                    "ms": unet_ms, "ms_per_forward": unet_ms / 256}
+                                    "ms": unet_ms, "ms_per_forward": unet_ms / 256,
+                                    "peak_sustained": F16_SUSTAINED_TFLOPS / 3,
+                                    "frac_sustained": ua / (F16_SUSTAINED_TFLOPS / 3)}
         print(json.dumps(rec), flush=True)
     if world > 1:
         import torch.distributed as dist
