@@ -50,6 +50,10 @@ static const Shape SHAPES[] = {
     {"L2 conv 384->384", 8, 16, 16, 384, 0, 384, 3, 1, 0},
     {"L3 conv 512->512", 8, 8, 8, 512, 0, 512, 3, 1, 0},
     {"L0 skip1x1 384->128", 8, 64, 64, 256, 128, 128, 1, 1, 0},
+    {"L1 skip1x1 640->256", 8, 32, 32, 384, 256, 256, 1, 1, 0},
+    {"L2 skip1x1 768->384", 8, 16, 16, 384, 384, 384, 1, 1, 0},
+    {"L3 skip1x1 1024->512", 8, 8, 8, 512, 512, 512, 1, 1, 0},
+    {"L1 proj 256->256", 8, 32, 32, 256, 0, 256, 1, 1, 0},
     {"L3 conv 1024->512", 8, 8, 8, 1024, 0, 512, 3, 1, 0},
     {"L2 conv 768->384", 8, 16, 16, 768, 0, 384, 3, 1, 0},
     {"L2 conv 896->384", 8, 16, 16, 896, 0, 384, 3, 1, 0},
@@ -178,6 +182,7 @@ int main(int argc, char** argv) {
         for (int v : variants) {
             const int BMv_[] = {128, 128, 256, 128, 64, 64, 64, 128, 64, 128}, BNv_[] = {128, 128, 128, 64, 128, 64, 64, 64, 128, 128};
             const int vb = v >= 10 ? 0 : v;
+            if (v == 30 && !splits_x) continue;
             const int BMv = v == 21 ? 128 : v >= 20 ? 256 : BMv_[vb], BNv = BNv_[vb];
             if ((v == 20 || v == 21) && !cfd::conv_h_tw(a)) continue;
             const int64_t tiles = ((M + BMv - 1) / BMv) * ((s.Cout + BNv - 1) / BNv);
@@ -192,7 +197,16 @@ int main(int argc, char** argv) {
             cfd::ConvArgs b = a;
             b.out = out1;
             b.xcd = 1;
+            // variant 30: the shipped K1s tiles of the planner's choice at CX_SPLITS splits
+            cfd::ConvPlan p30 = p;
+            p30.splits = splits;
+            p30.kx = -1;
+            if (v == 30 && p30.bm == 256) p30.bm = 128;
             auto run = [&]() {
+                if (v == 30) {
+                    cfd::launch_conv(b, p30, st, false);
+                    return;
+                }
                 cfd::launch_conv_x(b, v, splits, st);
                 if (splits > 1) cfd::launch_splitk_reduce(b, splits, st);
             };
