@@ -370,7 +370,12 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 template <int BM, int TW, int KG = 1>
 __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     constexpr int BN = 128, WGM = BM / 64, NTG = 64 * WGM * 2;   // threads per K group (the workgroup: NTG * KG)
-    constexpr int TR = BM / TW, HW2 = TW + 2, NPX = (TR + 2) * HW2;
+    // halo row stride HW2: TW + 2 columns, padded to a multiple of 4 where a
+    // 32-pixel fragment block spans two tile rows (TW = 16), so the second row's
+    // lanes keep the swizzle's bank pattern (PMC: 0.25 LDS bank-conflict rate
+    // unpadded); the pad columns load as zeros and are never read
+    constexpr int HW2 = TW < 32 ? (TW + 2 + 3) / 4 * 4 : TW + 2;
+    constexpr int TR = BM / TW, NPX = (TR + 2) * HW2;
     constexpr int HPLANE = NPX * 64;                  // one f16 plane of the halo (64 B per pixel)
     constexpr int HIT = (NPX * 8 + NTG - 1) / NTG;    // 16-B halo pieces per thread
     constexpr int BPLANE = BN * 64, BSTAGE = 2 * BPLANE;
@@ -416,7 +421,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
         if (hp < NPX) {
             const int hr = hp / HW2, hc = hp - hr * HW2;
             const int iy = y0 - 1 + hr, ix = x0 - 1 + hc;
-            if (iy >= 0 && iy < a.Hout && ix >= 0 && ix < W)
+            if (hc < TW + 2 && iy >= 0 && iy < a.Hout && ix >= 0 && ix < W)
                 pix = a.up ? (bimg * a.Hin + (iy >> 1)) * a.Win + (ix >> 1) : (bimg * a.Hin + iy) * a.Win + ix;
         }
         CFD_DASSERT(pix < srows);
