@@ -18,24 +18,40 @@ namespace cfd {
 
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// g = gamma * dz * SiLU'(z) (or gamma * dz), xhat = (x - mean) * rstd, for 4 channels
-__device__ __forceinline__ void gnb_load(const GnbArgs& a, int64_t pix, int64_t b, int c0, f4& g, f4& xh) {
-    const f4 x = c0 < a.C1 ? *(const f4*)(a.x1 + pix * a.C1 + c0) : *(const f4*)(a.x2 + pix * a.C2 + (c0 - a.C1));
-    f4 dz = *(const f4*)(a.dz + pix * a.Ctot + c0);
+// Per-thread constants of a channel quad c0..c0+3 of sample b: forward scale /
+// shift, gamma, group mean / rstd (loaded once, not per pixel).
+struct GnbQuad {
+    f4 sc, sh, gm, mean, rstd;
+};
+__device__ __forceinline__ GnbQuad gnb_quad(const GnbArgs& a, int64_t b, int c0) {
+    GnbQuad k;
     const int cpg = a.Ctot / 32;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int c = c0 + j;
-        const int grp = c / cpg;
-        const float mean = a.stats[(b * 32 + grp) * 2 + 0], rstd = a.stats[(b * 32 + grp) * 2 + 1];
+        const int c = c0 + j, grp = c / cpg;
+        k.sc[j] = a.ss[(b * a.Ctot + c) * 2 + 0];
+        k.sh[j] = a.ss[(b * a.Ctot + c) * 2 + 1];
+        k.gm[j] = a.gamma[c];
+        k.mean[j] = a.stats[(b * 32 + grp) * 2 + 0];
+        k.rstd[j] = a.stats[(b * 32 + grp) * 2 + 1];
+    }
+    return k;
+}
+
+// g = gamma * dz * SiLU'(z) (or gamma * dz), xhat = (x - mean) * rstd, for 4 channels
+__device__ __forceinline__ void gnb_load(const GnbArgs& a, const GnbQuad& k, int64_t pix, int c0, f4& g, f4& xh) {
+    const f4 x = c0 < a.C1 ? *(const f4*)(a.x1 + pix * a.C1 + c0) : *(const f4*)(a.x2 + pix * a.C2 + (c0 - a.C1));
+    f4 dz = *(const f4*)(a.dz + pix * a.Ctot + c0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
         float d = dz[j];
         if (a.silu) {
-            const float z = x[j] * a.ss[(b * a.Ctot + c) * 2 + 0] + a.ss[(b * a.Ctot + c) * 2 + 1];
+            const float z = x[j] * k.sc[j] + k.sh[j];
             const float sg = sigmoid_f(z);
             d = d * (sg * (1.0f + z * (1.0f - sg)));
         }
-        g[j] = d * a.gamma[c];
-        xh[j] = (x[j] - mean) * rstd;
+        g[j] = d * k.gm[j];
+        xh[j] = (x[j] - k.mean[j]) * k.rstd[j];
     }
 }
 
@@ -51,9 +67,10 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnbArgs a) {
     if (r0 < rows) {
         double s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
         const int c0 = 4 * q;
+        const GnbQuad k = gnb_quad(a, b, c0);
         for (int p = p0 + r0; p < p1; p += rows) {
             f4 g, xh;
-            gnb_load(a, b * HW + p, b, c0, g, xh);
+            gnb_load(a, k, b * HW + p, c0, g, xh);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 s[j] += g[j];
@@ -81,13 +98,14 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnbArgs a) {
     }
 }
 
-__global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(GnbArgs a) {
+// 32 threads per group, each summing every 32nd chunk, then a fixed-order tree
+__global__ __launch_bounds__(1024) void gn_bwd_finalize_kernel(GnbArgs a) {
     const int64_t b = blockIdx.x;
-    __shared__ double red[2][256];
+    __shared__ double red[2][1024];
+    const int grp = threadIdx.x >> 5, sub = threadIdx.x & 31;
     {
-        const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
         double s = 0, s2 = 0;
-        for (int ch = sub; ch < a.nchunks; ch += 8) {
+        for (int ch = sub; ch < a.nchunks; ch += 32) {
             const double* src = a.part + ((b * a.nchunks + ch) * 32 + grp) * 2;
             s += src[0];
             s2 += src[1];
@@ -96,44 +114,63 @@ __global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(GnbArgs a) {
         red[1][threadIdx.x] = s2;
     }
     __syncthreads();
-    if (threadIdx.x < 32) {
-        const int grp = threadIdx.x;
-        double s = 0, s2 = 0;
-        for (int k = 0; k < 8; ++k) {
-            s += red[0][grp * 8 + k];
-            s2 += red[1][grp * 8 + k];
+    for (int w = 16; w > 0; w >>= 1) {
+        if (sub < w) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + w];
+            red[1][threadIdx.x] += red[1][threadIdx.x + w];
         }
+        __syncthreads();
+    }
+    if (sub == 0) {
         const double n = (double)a.HW * (a.Ctot / 32);
-        a.fin[(b * 32 + grp) * 2 + 0] = (float)(s / n);
-        a.fin[(b * 32 + grp) * 2 + 1] = (float)(s2 / n);
+        a.fin[(b * 32 + grp) * 2 + 0] = (float)(red[0][threadIdx.x] / n);
+        a.fin[(b * 32 + grp) * 2 + 1] = (float)(red[1][threadIdx.x] / n);
     }
 }
 
+// thread = (channel quad, pixel); GNB_PIX pixels per thread at a stride of the
+// grid's pixel rows, so the per-channel constants load once per GNB_PIX pixels
+constexpr int GNB_PIX = 4;
 __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(GnbArgs a) {
     const int cq = a.Ctot / 4;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)a.B * a.HW * cq) return;
-    const int64_t pix = i / cq;
-    const int c0 = (int)(i - pix * cq) * 4;
-    const int64_t b = pix / a.HW;
-    f4 g, xh;
-    gnb_load(a, pix, b, c0, g, xh);
+    const int64_t npix = (int64_t)a.B * a.HW;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over (pixel row, quad)
+    const int64_t prow = i / cq;
+    const int c0 = (int)(i - prow * cq) * 4;
+    const int64_t nrow = (npix + GNB_PIX - 1) / GNB_PIX;
+    if (prow >= nrow) return;
     const int cpg = a.Ctot / 32;
-    f4 dx;
+    int64_t bcur = -1;
+    GnbQuad k;
+    f4 mg, mgx;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int grp = (c0 + j) / cpg;
-        const float rstd = a.stats[(b * 32 + grp) * 2 + 1];
-        const float mg = a.fin[(b * 32 + grp) * 2 + 0], mgx = a.fin[(b * 32 + grp) * 2 + 1];
-        dx[j] = rstd * (g[j] - mg - xh[j] * mgx);
-    }
-    if (a.addsrc) dx += *(const f4*)(a.addsrc + pix * a.Ctot + c0);
-    if (c0 < a.C1) {
-        f4* o = (f4*)(a.out1 + pix * a.C1 + c0);
-        *o = a.acc1 ? *o + dx : dx;
-    } else {
-        f4* o = (f4*)(a.out2 + pix * a.C2 + (c0 - a.C1));
-        *o = a.acc2 ? *o + dx : dx;
+    for (int e = 0; e < GNB_PIX; ++e) {
+        const int64_t pix = prow + e * nrow;
+        if (pix >= npix) break;
+        const int64_t b = pix / a.HW;
+        if (b != bcur) {
+            bcur = b;
+            k = gnb_quad(a, b, c0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int grp = (c0 + j) / cpg;
+                mg[j] = a.fin[(b * 32 + grp) * 2 + 0];
+                mgx[j] = a.fin[(b * 32 + grp) * 2 + 1];
+            }
+        }
+        f4 g, xh;
+        gnb_load(a, k, pix, c0, g, xh);
+        f4 dx;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dx[j] = k.rstd[j] * (g[j] - mg[j] - xh[j] * mgx[j]);
+        if (a.addsrc) dx += *(const f4*)(a.addsrc + pix * a.Ctot + c0);
+        if (c0 < a.C1) {
+            f4* o = (f4*)(a.out1 + pix * a.C1 + c0);
+            *o = a.acc1 ? *o + dx : dx;
+        } else {
+            f4* o = (f4*)(a.out2 + pix * a.C2 + (c0 - a.C1));
+            *o = a.acc2 ? *o + dx : dx;
+        }
     }
 }
 
@@ -326,9 +363,9 @@ void launch_gn_bwd(const GnbArgs& a0, int B, hipStream_t st) {
     a.B = B;
     hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
     check_launch("gn_bwd_partial_kernel");
-    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B), dim3(1024), 0, st, a);
     check_launch("gn_bwd_finalize_kernel");
-    const int64_t nq = (int64_t)B * a.HW * a.Ctot / 4;
+    const int64_t nq = ceil_div((int64_t)B * a.HW, GNB_PIX) * (a.Ctot / 4);
     hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a);
     check_launch("gn_bwd_apply_kernel");
 }
