@@ -76,17 +76,17 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(GnArgs a) {
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
 // per (b, c): scale = rstd*gamma, shift = beta - mean*scale (ATen CPU GroupNorm
-// affine form) from the chunk partials, summed in a fixed order.
-__global__ __launch_bounds__(256) void gn_finalize_kernel(GnArgs a) {
+// affine form) from the chunk partials: 32 threads per group each summing every
+// 32nd chunk, then a fixed-order tree (up to kGnMaxChunks chunks at large latents).
+__global__ __launch_bounds__(1024) void gn_finalize_kernel(GnArgs a) {
     const int64_t b = blockIdx.x;
     const int Ctot = a.Ctot, cpg = Ctot / 32;
     __shared__ float sh_mean[32], sh_rstd[32];
-    __shared__ double red[2][256];
-    // 8 threads per group, each summing every 8th chunk; then a fixed-order combine
+    __shared__ double red[2][1024];
+    const int grp = threadIdx.x >> 5, sub = threadIdx.x & 31;
     {
-        const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
         double s = 0, s2 = 0;
-        for (int ch = sub; ch < a.nchunks; ch += 8) {
+        for (int ch = sub; ch < a.nchunks; ch += 32) {
             const double* src = a.part + ((b * a.nchunks + ch) * 32 + grp) * 2;
             s += src[0];
             s2 += src[1];
@@ -95,16 +95,17 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnArgs a) {
         red[1][threadIdx.x] = s2;
     }
     __syncthreads();
-    if (threadIdx.x < 32) {
-        const int grp = threadIdx.x;
-        double s = 0, s2 = 0;
-        for (int k = 0; k < 8; ++k) {
-            s += red[0][grp * 8 + k];
-            s2 += red[1][grp * 8 + k];
+    for (int w = 16; w > 0; w >>= 1) {
+        if (sub < w) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + w];
+            red[1][threadIdx.x] += red[1][threadIdx.x + w];
         }
+        __syncthreads();
+    }
+    if (sub == 0) {
         const double n = (double)a.HW * cpg;
-        const double mean = s / n;
-        const double var = fmax(s2 / n - mean * mean, 0.0);
+        const double mean = red[0][threadIdx.x] / n;
+        const double var = fmax(red[1][threadIdx.x] / n - mean * mean, 0.0);
         sh_mean[grp] = (float)mean;
         sh_rstd[grp] = (float)(1.0 / sqrt(var + (double)a.eps));
         if (a.stats) {
@@ -114,10 +115,10 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnArgs a) {
     }
     __syncthreads();
     for (int c = threadIdx.x; c < Ctot; c += blockDim.x) {
-        const int grp = c / cpg;
-        const float sc = sh_rstd[grp] * a.gamma[c];
+        const int g = c / cpg;
+        const float sc = sh_rstd[g] * a.gamma[c];
         a.ss[(b * Ctot + c) * 2 + 0] = sc;
-        a.ss[(b * Ctot + c) * 2 + 1] = a.beta[c] - sh_mean[grp] * sc;
+        a.ss[(b * Ctot + c) * 2 + 1] = a.beta[c] - sh_mean[g] * sc;
     }
 }
 
@@ -1542,7 +1543,7 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     }
     hipLaunchKernelGGL(gn_partial_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
     check_launch("gn_partial_kernel");
-    hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(1024), 0, st, a);
     check_launch("gn_finalize_kernel");
     const int64_t nq = (int64_t)B * a.HW * a.Ctot / 4;
     hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a);
