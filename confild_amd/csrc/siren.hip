@@ -534,6 +534,253 @@ __global__ __launch_bounds__(64 * WAVES) void siren_tape_bwd(SirenTapeArgs p) {
     }
 }
 
+// K-split forms of the two tape kernels for small pair counts (a DPS step has
+// P = B x rows x sensors pairs, 3840 at Case4 B = 1: 240 waves of 16 pairs, a
+// quarter of the chip's SIMDs).  KS waves share one 16-pair tile and split each
+// layer's K (input features): wave w multiplies its quarter of the activations by
+// its quarter of every weight block (one block per step through the same LDS
+// ring) and parks the partial sum in LDS; the wave that owns the block's output
+// features (block j belongs to wave j / (NB/KS), which holds exactly those
+// features as its next-layer operand) adds the KS partials in wave order, takes
+// the sine (forward) or the cos derivative (backward) and writes the tape.  Same
+// products as the one-wave kernels, partial sums added in a fixed order
+// (deterministic, batch invariant); KS x the waves per pair tile.
+template <int NB, int KS>
+__global__ __launch_bounds__(64 * KS) void siren_tape_fwd_ks(SirenTapeArgs p) {
+    constexpr int H = NB * 16, BLK = NB * 256, QW = NB / KS;
+    static_assert(NB % KS == 0, "K split must divide the blocks");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* wbuf = smem;               // 2 ring slots
+    float* w0s = smem + 2 * BLK;      // (H, 4)
+    float* red = w0s + 4 * H;         // 2 x KS x 64 lanes x f4 partial sums
+    float* osum = red + 2 * KS * 256; // KS x 4 x 16
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int64_t row = nc / p.Ns;
+    const int sensor = (int)(nc - row * p.Ns);
+    const int nh = p.nh, nl = nh + 1;
+    const float* film = p.film + row * nl * H;
+    float* ut = p.u + nc * nl * H;
+    const bool live = n < p.P;
+    const int q0 = wave * QW;
+
+    for (int f = threadIdx.x; f < H; f += 64 * KS) {
+        f4 w = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < p.d; ++k) w[k] = p.w0[f * p.d + k];
+        *(f4*)(w0s + 4 * f) = w;
+    }
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < p.d) {
+            float v = p.coords[(int64_t)sensor * p.d + k];
+            if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+            cn[k] = v;
+        }
+    }
+    __syncthreads();
+    if (nh > 0) siren_issue_block<NB, KS>(p.wimg, 0, wbuf, wave, lane);
+
+    float X[QW][4], Xn[QW][4];
+    static_for<QW>([&](auto qc) {
+        constexpr int qq = decltype(qc)::value;
+        const int q = q0 + qq;
+        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
+        f4 uu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
+            float a = cn[0] * w[0];
+#pragma unroll
+            for (int k = 1; k < 4; ++k)
+                if (k < p.d) a = fmaf(cn[k], w[k], a);
+            uu[r] = a + fv[r];
+            X[qq][r] = sin_cw(p.w0f * uu[r]);
+        }
+        if (live) *(f4*)(ut + 16 * q + 4 * g) = uu;
+    });
+
+    const int nblocks = nh * NB;
+    int J = 0;
+    for (int layer = 1; layer <= nh; ++layer) {
+        static_for<NB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (J + 1 < nblocks) siren_issue_block<NB, KS>(p.wimg, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            const float* wb = wbuf + (J & 1) * BLK;
+            f4 a = wave == 0 ? *(const f4*)(film + layer * H + 16 * j + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
+            static_for<QW>([&](auto qc) {
+                constexpr int qq = decltype(qc)::value;
+                const f4 w = *(const f4*)(wb + ((q0 + qq) * 64 + lane) * 4);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, X[qq][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, X[qq][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, X[qq][2], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, X[qq][3], a, 0, 0, 0);
+            });
+            float* rs = red + (j & 1) * KS * 256;
+            *(f4*)(rs + (wave * 64 + lane) * 4) = a;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (j / QW == wave) {   // this wave owns output block j: its next-layer features
+                constexpr int qq = j % QW;
+                f4 acc = *(const f4*)(rs + lane * 4);
+#pragma unroll
+                for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+                if (live) *(f4*)(ut + layer * H + 16 * j + 4 * g) = acc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Xn[qq][r] = sin_cw(p.w0f * acc[r]);
+            }
+            ++J;
+        });
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[qq][r] = Xn[qq][r];
+        });
+    }
+
+    // output layer: partial sums over this wave's features, combined in wave order
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            const float* wr = p.wout + oc * H + 4 * g;
+            float sm = 0.f;
+            static_for<QW>([&](auto qc) {
+                constexpr int qq = decltype(qc)::value;
+                const f4 w = *(const f4*)(wr + 16 * (q0 + qq));
+                sm = fmaf(w.x, X[qq][0], sm);
+                sm = fmaf(w.y, X[qq][1], sm);
+                sm = fmaf(w.z, X[qq][2], sm);
+                sm = fmaf(w.w, X[qq][3], sm);
+            });
+            sm += __shfl_xor(sm, 16);
+            sm += __shfl_xor(sm, 32);
+            if (g == 0) osum[(wave * 4 + oc) * 16 + j16] = sm;
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            float sm = osum[oc * 16 + j16];
+#pragma unroll
+            for (int w = 1; w < KS; ++w) sm += osum[(w * 4 + oc) * 16 + j16];
+            o[oc] = sm + p.bout[oc];
+        }
+    }
+    if (live && g < p.c) {
+        float v = g == 0 ? o[0] : g == 1 ? o[1] : g == 2 ? o[2] : o[3];
+        if (p.ymax) {
+            const int64_t yi = (int64_t)sensor * p.ystride + g;
+            const float hi = p.ymax[yi], lo = p.ymin[yi];
+            v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
+        }
+        p.out[n * p.c + g] = v;
+    }
+}
+
+template <int NB, int KS>
+__global__ __launch_bounds__(64 * KS) void siren_tape_bwd_ks(SirenTapeArgs p) {
+    constexpr int H = NB * 16, BLK = NB * 256, QW = NB / KS;
+    static_assert(NB % KS == 0, "K split must divide the blocks");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* wbuf = smem;
+    float* red = smem + 2 * BLK;      // 2 x KS x 64 lanes x f4
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int sensor = (int)(nc % p.Ns);
+    const int nh = p.nh, nl = nh + 1;
+    const float* ut = p.u + nc * nl * H;
+    float* dt = p.delta + nc * nl * H;
+    const bool live = n < p.P;
+    const float w0f = p.w0f;
+    const int q0 = wave * QW;
+
+    if (nh > 0) siren_issue_block<NB, KS>(p.wimg_t, 0, wbuf, wave, lane);
+    float dy[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            float v = live ? p.gout[nc * p.c + oc] : 0.f;
+            if (p.ymax) {
+                const int64_t yi = (int64_t)sensor * p.ystride + oc;
+                v = v * ((p.ymax[yi] - p.ymin[yi]) / 2.0f);
+            }
+            dy[oc] = v;
+        }
+    }
+    float X[QW][4], Xn[QW][4];
+    static_for<QW>([&](auto qc) {
+        constexpr int qq = decltype(qc)::value;
+        const int q = q0 + qq;
+        const f4 uu = *(const f4*)(ut + nh * H + 16 * q + 4 * g);
+        f4 dd;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = 16 * q + 4 * g + r;
+            float gx = 0.f;
+#pragma unroll
+            for (int oc = 0; oc < 4; ++oc)
+                if (oc < p.c) gx = fmaf(p.wout[oc * H + f], dy[oc], gx);
+            dd[r] = gx * (w0f * cos_cw(w0f * uu[r]));
+            X[qq][r] = dd[r];
+        }
+        if (live) *(f4*)(dt + nh * H + 16 * q + 4 * g) = dd;
+    });
+
+    const int nblocks = nh * NB;
+    int J = 0;
+    for (int layer = nh; layer >= 1; --layer) {
+        const int li = layer - 1;
+        static_for<NB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (J + 1 < nblocks)
+                siren_issue_block<NB, KS>(p.wimg_t, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            const float* wb = wbuf + (J & 1) * BLK;
+            f4 a = {0.f, 0.f, 0.f, 0.f};
+            static_for<QW>([&](auto qc) {
+                constexpr int qq = decltype(qc)::value;
+                const f4 w = *(const f4*)(wb + ((q0 + qq) * 64 + lane) * 4);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, X[qq][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, X[qq][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, X[qq][2], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, X[qq][3], a, 0, 0, 0);
+            });
+            float* rs = red + (j & 1) * KS * 256;
+            *(f4*)(rs + (wave * 64 + lane) * 4) = a;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (j / QW == wave) {
+                constexpr int qq = j % QW;
+                f4 acc = *(const f4*)(rs + lane * 4);
+#pragma unroll
+                for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+                const f4 uu = *(const f4*)(ut + li * H + 16 * j + 4 * g);
+                f4 dd;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    dd[r] = acc[r] * (w0f * cos_cw(w0f * uu[r]));
+                    Xn[qq][r] = dd[r];
+                }
+                if (live) *(f4*)(dt + li * H + 16 * j + 4 * g) = dd;
+            }
+            ++J;
+        });
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[qq][r] = Xn[qq][r];
+        });
+    }
+}
+
 // g_z[r][l] = sum_i sum_f V_i[f][l] * (sum_s delta[r*Ns + s][i][f])
 __global__ __launch_bounds__(256) void siren_latent_grad(const float* __restrict__ delta,
                                                          const float* __restrict__ V, float* __restrict__ gz,
@@ -951,8 +1198,27 @@ void launch_tape_w(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
     cfd::check_launch(bwd ? "siren_tape_bwd" : "siren_tape_fwd");
 }
 
+template <int NB, int KS>
+void launch_tape_ks(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
+    const size_t lds = sizeof(float) * (2 * NB * 256 + 2 * KS * 256 + (bwd ? 0 : 4 * NB * 16 + KS * 64));
+    const void* fn = bwd ? (const void*)cfd::siren_tape_bwd_ks<NB, KS> : (const void*)cfd::siren_tape_fwd_ks<NB, KS>;
+    CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const dim3 grid((unsigned)cfd::ceil_div(a.P, 16));
+    if (bwd)
+        hipLaunchKernelGGL((cfd::siren_tape_bwd_ks<NB, KS>), grid, dim3(64 * KS), lds, st, a);
+    else
+        hipLaunchKernelGGL((cfd::siren_tape_fwd_ks<NB, KS>), grid, dim3(64 * KS), lds, st, a);
+    cfd::check_launch(bwd ? "siren_tape_bwd_ks" : "siren_tape_fwd_ks");
+}
+
 template <int NB>
 void launch_tape_nb(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
+    // K-split tiles where one wave per 16 pairs leaves most SIMDs idle
+    // (CFD_SIREN_TAPE_KS=0: the one-wave-per-tile kernels everywhere)
+    static const int ks_env = getenv("CFD_SIREN_TAPE_KS") ? atoi(getenv("CFD_SIREN_TAPE_KS")) : 1;
+    if constexpr (NB % 4 == 0 && NB <= 24) {
+        if (ks_env && a.P < 16 * 2048) return launch_tape_ks<NB, 4>(a, bwd, st);
+    }
     switch (tape_waves(a.P)) {
         case 4: return launch_tape_w<NB, 4>(a, bwd, st);
         case 2: return launch_tape_w<NB, 2>(a, bwd, st);

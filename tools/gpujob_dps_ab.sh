@@ -1,11 +1,10 @@
-# DPS GPU tests (split-f16 input-VJP), then a same-box A/B of the DPS step:
-# split-f16 transposed convolutions (default) vs fp32 (CFD_VJP_SPLIT=0).
+# same-box A/B of an environment switch on the DPS benches (config D, Case4 B=1 and B=8)
+#   bash tools/gpujob_dps_ab.sh "ENV_A=.." "ENV_B=.."
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_dps.py tests/test_gpu_e2e.py -x -q --timeout 200 --timeout-method thread > gpurun_out/dps_tests.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/dps_tests.log; exit 1; }
-tail -1 gpurun_out/dps_tests.log
-for r in 1 2; do
-for V in CFD_VJP_SPLIT=1 CFD_VJP_SPLIT=0; do
-env $V timeout -k 10 200 python tools/kbench.py dps > gpurun_out/kb_d.log 2>&1 || { cat gpurun_out/kb_d.log; exit 2; }
-echo "$V $(tail -1 gpurun_out/kb_d.log | cut -c1-400)"
-done; done
+for E in "$1" "$2"; do
+  env $E timeout -k 10 300 python3 bench.py --config D --steps 1 --warmup 1 > gpurun_out/ab_d.json 2> gpurun_out/ab.err || { tail gpurun_out/ab.err; exit 1; }
+  env $E timeout -k 10 300 python3 bench.py --config Case4 --dps-steps 50 --steps 1 --warmup 1 > gpurun_out/ab_c1.json 2> gpurun_out/ab.err || { tail gpurun_out/ab.err; exit 2; }
+  env $E timeout -k 10 400 python3 bench.py --config Case4 --dps-steps 30 --batch 8 --steps 1 --warmup 1 > gpurun_out/ab_c8.json 2> gpurun_out/ab.err || { tail gpurun_out/ab.err; exit 3; }
+  echo "$E D $(python3 -c "import json;print(round(json.load(open('gpurun_out/ab_d.json'))['value'],1))") it/s, Case4 B=1 $(python3 -c "import json;print(round(json.load(open('gpurun_out/ab_c1.json'))['value'],2))"), B=8 $(python3 -c "import json;print(round(json.load(open('gpurun_out/ab_c8.json'))['value'],2))")"
+done
