@@ -115,8 +115,6 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats);
 // launched: the caller runs launch_splitk_reduce or hands the slab to launch_gn.
 int launch_conv(const ConvArgs& a, const ConvPlan& p, hipStream_t st, bool defer = false);
 void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st);
-// K1x (conv_x.hip): split-f16 forward convolution on 32x32x16 MFMAs with 64x64
-// wave tiles and an in-workgroup K split; variant selects the tile shape
 // Workgroup -> (m tile, n tile, split) in XCD-contiguous order (the hardware
 // deals workgroups round-robin over the 8 XCDs): XCD x gets the x-th contiguous
 // run of tiles.  order 1: splits fastest, then n, then m (the workgroups of an
@@ -142,6 +140,8 @@ __device__ __forceinline__ void xcd_tile(int order, int& bx, int& by, int& bz) {
         bx = Lp / (gz * gy);
     }
 }
+// K1x / K1h (conv_x.hip): split-f16 forward convolutions on 32x32x16 MFMAs with
+// 64x64 wave tiles; variant selects the kernel and tile shape
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st);
 int conv_h_tw(const ConvArgs& a);   // K1h tile width for a shape, 0: not applicable
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
