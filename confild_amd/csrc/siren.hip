@@ -828,6 +828,8 @@ struct cfd_siren {
     float* wimg16 = nullptr; // split-f16 image (hi, lo) of the scaled hidden weights, same bytes as wimg
     float* wscale = nullptr; // (nh) power-of-two scale of each hidden layer in wimg16
     float* wimg32 = nullptr; // the same split in the 32x32x16 chain's k order (siren_split32)
+    float* wimg32r = nullptr; // siren_split32 image of W (w0 / 2pi) s'_i: accumulators in revolutions
+    float* wrev = nullptr;    // (2 nh): (w0 / 2pi) s'_i, then 1 / s'_i
     int compute = CFD_SIREN_SPLIT_F16;
 };
 
@@ -932,6 +934,35 @@ void pack_split_f16(cfd_siren* h, int li, const float* W) {
                     }
         CFD_HIP(hipMemcpy(h->wimg32 + (size_t)(li - 1) * NB * NB * 256, img.data(),
                           img.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+        // the same image of W (w0 / 2pi) s'_i (s'_i = 2^-e, e the frexp exponent of
+        // max|W w0 / 2pi|; scaled and split from float64, both halves RNE): the
+        // accumulator of s'_i F_i (w0 / 2pi) + sum is the pre-activation in
+        // revolutions times s'_i, so the sine is one multiply by 1/s'_i (exact),
+        // a fract and v_sin_f32 (siren_split32, HWSIN >= 3)
+        const double kr = (double)h->cfg.w0 / (2.0 * M_PI);
+        const double amr = (double)amax * kr;
+        int er = 0;
+        if (amr > 0.0) std::frexp(amr, &er);
+        const double sr = std::ldexp(1.0, -er);
+        for (int J = 0; J < NB2; ++J)
+            for (int k = 0; k < NK; ++k)
+                for (int l = 0; l < 64; ++l)
+                    for (int t = 0; t < 8; ++t) {
+                        const int jb = k / 2, e = k % 2;
+                        const double v = (double)W[(size_t)(32 * J + l % 32) * H + 32 * jb + 8 * (2 * e + t / 4) +
+                                                   4 * (l / 32) + t % 4] * kr * sr;
+                        const _Float16 hi = (_Float16)v;
+                        const _Float16 lo = (_Float16)(v - (double)hi);
+                        const size_t base = ((size_t)J * NK + k) * 1024 + l * 8 + t;
+                        img[base] = hi;
+                        img[base + 512] = lo;
+                    }
+        CFD_HIP(hipMemcpy(h->wimg32r + (size_t)(li - 1) * NB * NB * 256, img.data(),
+                          img.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+        const int nh = h->cfg.num_hidden_layers;
+        const float fs = (float)(kr * sr), inv = (float)(1.0 / sr);
+        CFD_HIP(hipMemcpy(h->wrev + (li - 1), &fs, sizeof(float), hipMemcpyHostToDevice));
+        CFD_HIP(hipMemcpy(h->wrev + nh + (li - 1), &inv, sizeof(float), hipMemcpyHostToDevice));
     }
     CFD_HIP(hipMemcpy(h->wscale + (li - 1), &s, sizeof(float), hipMemcpyHostToDevice));
 }
@@ -973,6 +1004,8 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_HIP(hipMalloc(&h->wimg16, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wscale, sizeof(float) * (size_t)std::max(nh, 1)));
         CFD_HIP(hipMalloc(&h->wimg32, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
+        CFD_HIP(hipMalloc(&h->wimg32r, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
+        CFD_HIP(hipMalloc(&h->wrev, sizeof(float) * 2 * (size_t)std::max(nh, 1)));
         if (const char* e = getenv("CFD_SIREN_COMPUTE")) h->compute = atoi(e);
         *out = h;
     });
@@ -990,6 +1023,8 @@ extern "C" void cfd_siren_destroy(cfd_siren* h) {
     (void)hipFree(h->wimg16);
     (void)hipFree(h->wscale);
     (void)hipFree(h->wimg32);
+    (void)hipFree(h->wimg32r);
+    (void)hipFree(h->wrev);
     delete h;
 }
 
@@ -1132,6 +1167,8 @@ extern "C" int cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, c
             }();
             if (use32 && cfd::siren_split32_supported(H, nh)) {
                 a.wimg = h->wimg32;
+                a.wimg_rev = h->wimg32r;
+                a.wrev = h->wrev;
                 cfd::launch_siren_split32(H, a, b, st);
             } else {
                 a.wimg = h->wimg16;

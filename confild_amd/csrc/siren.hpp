@@ -32,6 +32,8 @@ struct SirenArgs {
     const float* ymin;
     float* out;           // (b, N, c)
     const float* wscale;  // (nh) power-of-two weight scale of each hidden layer (split-f16 image only)
+    const float* wimg_rev; // siren_split32 image of the hidden weights pre-scaled by (w0 / 2pi) s'_i (HWSIN >= 3)
+    const float* wrev;     // (2 nh): FiLM scale (w0 / 2pi) s'_i of each hidden layer, then 1 / s'_i
     int64_t N;
     int64_t ystride;
     int64_t b0;           // first latent of this launch (grid.y chunking)

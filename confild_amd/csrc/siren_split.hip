@@ -141,6 +141,23 @@ __device__ __forceinline__ float sin_hw_rev(float x) {
     return __builtin_amdgcn_sinf(r);
 }
 
+// The hidden-layer sine of siren_split32.  HWSIN 0-2: x is the pre-activation
+// w0 u in radians (sin1_cw / sin_hw / sin_hw_rev).  HWSIN 3 and 4: the weights and
+// FiLM rows carry w0 / 2pi (wimg_rev), so x = u w0 / 2pi is already in
+// revolutions.  4, the default: v_sin_f32 on x as it is -- its input reduction is
+// exact (probed over |x| < 1e7 rev: max abs error 1.2e-7, the same as on |x| <= 16;
+// test_device_sine_in_revolutions), so the sine costs no VALU besides the
+// transcendental (sin_hw_rev: 4 + 1).  3: an explicit r = fract(x) first (fract of a
+// small negative x rounds 1 + x to 2^-24: 3.7e-7).
+template <int HWSIN>
+__device__ __forceinline__ float hidden_sine(float x) {
+    if constexpr (HWSIN == 4) return __builtin_amdgcn_sinf(x);
+    else if constexpr (HWSIN == 3) return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(x));
+    else if constexpr (HWSIN == 2) return sin_hw_rev(x);
+    else if constexpr (HWSIN == 1) return sin_hw(x);
+    else return sin1_cw(x);
+}
+
 template <bool PK>
 __device__ __forceinline__ f2 sin2_sel(f2 x) {
     if constexpr (PK) return sin2_cw(x);
@@ -476,8 +493,9 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
         const int nf = (nh + 1) * H;
         for (int i = threadIdx.x * 4; i < nf; i += 64 * WAVES * 4) {
             const int layer = i / H;
-            const float sc = layer == 0 ? 1.0f : p.wscale[layer - 1];
-            *(f4*)(film + i) = *(const f4*)(fsrc + i) * sc;  // power-of-two: exact
+            // HWSIN < 3: power-of-two s_i (exact); HWSIN >= 3: (w0 / 2pi) s'_i
+            const float sc = layer == 0 ? 1.0f : HWSIN >= 3 ? p.wrev[layer - 1] : p.wscale[layer - 1];
+            *(f4*)(film + i) = *(const f4*)(fsrc + i) * sc;
         }
     }
     for (int f = threadIdx.x; f < H; f += 64 * WAVES) {
@@ -522,7 +540,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
 #pragma unroll
                 for (int k = 1; k < 4; ++k)
                     if (k < p.d) a = fmaf(cn[k], w[k], a);
-                x[4 * qq + r] = HWSIN == 2 ? sin_hw_rev(p.w0f * (a + fv[r])) : HWSIN ? sin_hw(p.w0f * (a + fv[r])) : sin1_cw(p.w0f * (a + fv[r]));
+                x[4 * qq + r] = hidden_sine<HWSIN >= 2 ? 2 : HWSIN>(p.w0f * (a + fv[r]));
             }
         }
         split_chunk(x, 0, NH[2 * J], NL[2 * J]);
@@ -543,7 +561,8 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
     float x[16];
     for (int layer = 1; layer <= nh; ++layer) {
         const bool last = layer == nh;
-        const float m = p.w0f / p.wscale[layer - 1];  // power-of-two scale: exact
+        // power-of-two scales: exact (HWSIN >= 3: 1 / s'_i, the result in revolutions)
+        const float m = HWSIN >= 3 ? p.wrev[nh + layer - 1] : p.w0f / p.wscale[layer - 1];
         // output-layer partial sums over the 4 features of part e of block jp (x: its sines)
         auto outsum = [&](int jp, int e) __attribute__((always_inline)) {  // wos rows oc >= c are zero
             const int f = 32 * jp + 8 * e + 4 * h;
@@ -604,7 +623,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
                 if constexpr (k < NKS) {
 #pragma unroll
                     for (int v = 16 * k / NKS; v < 16 * (k + 1) / NKS; ++v) {
-                        x[v] = (EXP & 2) ? prev[v] * me : HWSIN == 2 ? sin_hw_rev(prev[v] * me) : HWSIN ? sin_hw(prev[v] * me) : sin1_cw(prev[v] * me);
+                        x[v] = (EXP & 2) ? prev[v] * me : hidden_sine<HWSIN>(prev[v] * me);
                         asm volatile("" : "+v"(x[v]));  // keep it in this step (no sinking to the split)
                     }
                 }
@@ -642,7 +661,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
     }
     // the last layer's last block
 #pragma unroll
-    for (int v = 0; v < 16; ++v) x[v] = HWSIN == 2 ? sin_hw_rev(prev[v] * mprev) : HWSIN ? sin_hw(prev[v] * mprev) : sin1_cw(prev[v] * mprev);
+    for (int v = 0; v < 16; ++v) x[v] = hidden_sine<HWSIN>(prev[v] * mprev);
     {
         const int f0 = 32 * (NB2 - 1) + 4 * h;
 #pragma unroll
@@ -753,7 +772,18 @@ bool siren_split32_supported(int H, int nh) {
 }
 
 void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
-    static const int hw = env_int("CFD_SIREN_HWSIN", 2, 0, 2);
+    static const int hw = env_int("CFD_SIREN_HWSIN", 4, 0, 4);
+    if (hw >= 3) {
+        CFD_REQUIRE(a.wimg_rev && a.wrev, CFD_EARG, "split32 revolution image not set");
+        a.wimg = a.wimg_rev;
+        switch (H) {
+            case 64: return hw == 3 ? launch_split32<2, 0, 3>(a, b, st) : launch_split32<2, 0, 4>(a, b, st);
+            case 128: return hw == 3 ? launch_split32<4, 0, 3>(a, b, st) : launch_split32<4, 0, 4>(a, b, st);
+            case 256: return hw == 3 ? launch_split32<8, 0, 3>(a, b, st) : launch_split32<8, 0, 4>(a, b, st);
+            case 384: return hw == 3 ? launch_split32<12, 0, 3>(a, b, st) : launch_split32<12, 0, 4>(a, b, st);
+            default: break;
+        }
+    }
     if (hw) {
         switch (H) {
             case 64: return hw == 2 ? launch_split32<2, 0, 2>(a, b, st) : launch_split32<2, 0, 1>(a, b, st);
@@ -802,14 +832,19 @@ void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st) {
 
 __global__ void sine_probe_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int which) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) y[i] = which == 2 ? sin_hw_rev(x[i]) : which == 1 ? sin_hw(x[i]) : sin1_cw(x[i]);
+    if (i < n)
+        y[i] = which == 4   ? hidden_sine<4>(x[i])
+               : which == 3 ? hidden_sine<3>(x[i])
+               : which == 2 ? sin_hw_rev(x[i])
+               : which == 1 ? sin_hw(x[i])
+                            : sin1_cw(x[i]);
 }
 
 }  // namespace cfd
 
 extern "C" int cfd_sine_probe(const float* x, float* y, int64_t n, int which, void* stream) {
     return cfd::guard([&] {
-        CFD_REQUIRE(x && y && n > 0 && which >= 0 && which <= 2, CFD_EARG, "bad argument");
+        CFD_REQUIRE(x && y && n > 0 && which >= 0 && which <= 4, CFD_EARG, "bad argument");
         hipLaunchKernelGGL(cfd::sine_probe_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0,
                            (hipStream_t)stream, x, y, n, which);
         cfd::check_launch("sine_probe_kernel");

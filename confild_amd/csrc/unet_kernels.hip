@@ -1055,8 +1055,14 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 // of two 16-key S^T tiles, so P^T feeds the P.V MFMA straight from the softmax
 // registers.  attention_split_kernel then runs S^T = K Q^T and O^T = V^T P^T as
 // three v_mfma_f32_16x16x32_f16 each (lo*hi + hi*lo + hi*hi, fp32 accumulate) over
-// 32-key blocks with the fp32 kernel's online softmax.
+// 32-key blocks with the fp32 kernel's online softmax.  K carries the q/k scale
+// times log2(e) (kln2 below), so S is in base-2 units: every exponential is one
+// v_exp_f32 (ocml's expf is ~11 instructions: the softmax was ~1/3 of the loop's
+// issue) and the saved log-sum-exp is converted back to natural units.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ float kln2(float scale) { return scale * 1.44269504088896340736f; }
+// s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
+constexpr int vmcnt_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
 __device__ __forceinline__ void split8_f16(const float (&v)[8], h8v& hi, h8v& lo) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -1089,8 +1095,9 @@ __global__ __launch_bounds__(256) void attn_kv_split_kernel(AttnArgs a, int CH, 
         const int kt = (int)(f / nj), j = (int)(f - (int64_t)kt * nj);
         const int key = 16 * kt + li;
         const float* kp = base + (int64_t)min(key, T - 1) * C3 + CH + 32 * j + 8 * g;
+        const float ks = kln2(a.scale);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = key < T ? kp[t] * a.scale : 0.f;
+        for (int t = 0; t < 8; ++t) v[t] = key < T ? kp[t] * ks : 0.f;
         dst = kf + ((bh * (T32 / 16) + kt) * nj + j) * 128 + lane;
         stride = 64;
     } else {
@@ -1180,23 +1187,27 @@ __global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const 
         for (int z = 0; z < QT; ++z) {
             // lane (g, li) holds S[query li][key kb + 16u + 4g + r]
             float mx = -INFINITY;
+            if (kb + 32 > T) {   // the ragged last block only (wave-uniform)
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (kb + 16 * u + 4 * g + r >= T) st[z][u][r] = -INFINITY;
+            }
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if (kb + 16 * u + 4 * g + r >= T) st[z][u][r] = -INFINITY;
-                    mx = fmaxf(mx, st[z][u][r]);
-                }
+                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[z][u][r]);
             mx = fmaxf(mx, __shfl_xor(mx, 16));
             mx = fmaxf(mx, __shfl_xor(mx, 32));
             const float mnew = fmaxf(mrun[z], mx);
-            const float alpha = expf(mrun[z] - mnew);
+            const float alpha = __builtin_amdgcn_exp2f(mrun[z] - mnew);   // S in base-2 units
             float p[8], ps = 0.f;
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    p[4 * u + r] = expf(st[z][u][r] - mnew);
+                    p[4 * u + r] = __builtin_amdgcn_exp2f(st[z][u][r] - mnew);
                     ps += p[4 * u + r];
                 }
             ps += __shfl_xor(ps, 16);
@@ -1225,7 +1236,8 @@ __global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const 
 #pragma unroll
     for (int z = 0; z < QT; ++z) {
         const int tq = q0 + 16 * z + li;
-        if (a.lse && g == 0 && tq < T) a.lse[((int64_t)b * gridDim.y + h) * T + tq] = mrun[z] + logf(lrun[z]);
+        if (a.lse && g == 0 && tq < T)   // natural units (the backward's exp(S - lse))
+            a.lse[((int64_t)b * gridDim.y + h) * T + tq] = (mrun[z] + log2f(lrun[z])) * 0.69314718055994530942f;
         if (tq < T) {
             float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
             const float inv = 1.0f / lrun[z];
@@ -1234,6 +1246,151 @@ __global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const 
                 f4 v = O[z][d] * inv;
                 *(f4*)(op + 16 * d + 4 * g) = v;
             }
+        }
+    }
+}
+
+// K4d: attention_split_kernel with each 32-key block's packed K/V fragments
+// (attn_kv_split's layout: K of the block's two 16-key tiles = 4 NJ contiguous
+// 1-KiB pieces, V = 2 ND pieces) staged ONCE per workgroup into an NS-stage LDS
+// ring by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no VALU), NS - 1
+// blocks in flight, one barrier per block.  K4s has every wave stream the whole
+// K/V of its (sample, head) from L2 for its 16 queries (1 GB of L2 reads per
+// 32^2 attention at config B, the loop's bound: cutting its instruction count by
+// 45% left it unchanged); here WAVES waves share one copy.  Fragments, MFMA order
+// and softmax are K4s', so the output is bit-identical to it.
+template <int CH, int WAVES, int NS = 3>
+__global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, const h8v* __restrict__ kf,
+                                                                   const h8v* __restrict__ vf) {
+    constexpr int NJ = CH / 32, ND = CH / 16;
+    constexpr int KP = 4 * NJ, NP = KP + 2 * ND;   // 1-KiB pieces per block: K, then V
+    constexpr int PPW = NP / WAVES;                // pieces per wave and block
+    static_assert(NP % WAVES == 0 && NS >= 2 && NS <= 3, "piece split");
+    __shared__ __attribute__((aligned(16))) h8v ring[NS][NP * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, li = lane & 15;
+    const int h = blockIdx.y, heads = gridDim.y;
+    const int64_t b = blockIdx.z;
+    const int T = a.T, T32 = (T + 31) / 32 * 32;
+    const int q0 = (blockIdx.x * WAVES + wave) * 16;
+    const bool active = q0 < T;   // wave-uniform; an idle wave still stages and syncs
+    CFD_DASSERT(h * CH + CH <= a.C);
+    const int C3 = 3 * a.C;
+    const float* base = a.qkv + b * (int64_t)T * C3 + (int64_t)h * 3 * CH;
+    const int64_t bh = b * heads + h;
+    const h8v* kfb = kf + bh * (T32 / 16) * NJ * 128;
+    const h8v* vfb = vf + bh * (T32 / 32) * ND * 128;
+    auto issue = [&](int kb, int stage) {
+        const h8v* ks = kfb + (int64_t)(kb >> 4) * NJ * 128;
+        const h8v* vs = vfb + (int64_t)(kb >> 5) * ND * 128;
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            const int piece = wave + WAVES * i;
+            const h8v* src = piece < KP ? ks + piece * 64 : vs + (piece - KP) * 64;
+            __builtin_amdgcn_global_load_lds((const void*)(src + lane),
+                                             (__attribute__((address_space(3))) void*)&ring[stage][piece * 64], 16, 0, 0);
+        }
+    };
+    const int nblk = T32 / 32;
+#pragma unroll
+    for (int i = 0; i < NS - 1; ++i)
+        if (i < nblk) issue(32 * i, i);
+
+    h8v qh[NJ], ql[NJ];
+    {
+        const int tq = min(q0 + li, T - 1);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const float* qp = base + (int64_t)tq * C3 + 32 * j + 8 * g;
+            float v[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] = qp[t] * a.scale;
+            split8_f16(v, qh[j], ql[j]);
+        }
+    }
+    f4 O[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) O[d] = f4{0.f, 0.f, 0.f, 0.f};
+    float mrun = -INFINITY, lrun = 0.f;
+
+    for (int ib = 0; ib < nblk; ++ib) {
+        const int kb = 32 * ib, stage = ib % NS;
+        // this wave's pieces of block ib landed (the blocks issued after it may
+        // still fly), then the barrier publishes every wave's pieces and retires
+        // every read of the stage refilled below (block ib - 1's)
+        if (NS == 3 && ib + 1 < nblk)
+            __builtin_amdgcn_s_waitcnt(vmcnt_wait(PPW));
+        else
+            __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
+        __builtin_amdgcn_s_barrier();
+        if (ib + NS - 1 < nblk) issue(kb + 32 * (NS - 1), (ib + NS - 1) % NS);
+        if (!active) continue;
+        const h8v* kl8 = &ring[stage][lane];
+        f4 st[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            st[u] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const h8v kh = kl8[((u * NJ + j) * 2) * 64], kl = kl8[((u * NJ + j) * 2 + 1) * 64];
+                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qh[j], st[u], 0, 0, 0);
+                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, ql[j], st[u], 0, 0, 0);
+                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[j], st[u], 0, 0, 0);
+            }
+        }
+        float mx = -INFINITY;
+        if (kb + 32 > T) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (kb + 16 * u + 4 * g + r >= T) st[u][r] = -INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[u][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(mrun, mx);
+        const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
+        float p[8], ps = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                p[4 * u + r] = __builtin_amdgcn_exp2f(st[u][r] - mnew);
+                ps += p[4 * u + r];
+            }
+        ps += __shfl_xor(ps, 16);
+        ps += __shfl_xor(ps, 32);
+        lrun = lrun * alpha + ps;
+        mrun = mnew;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) O[d] = O[d] * alpha;
+        h8v ph, pl;
+        split8_f16(p, ph, pl);
+        const h8v* vl8 = &ring[stage][KP * 64 + lane];
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            const h8v vh = vl8[(2 * d) * 64], vl = vl8[(2 * d + 1) * 64];
+            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, O[d], 0, 0, 0);
+            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, O[d], 0, 0, 0);
+            O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, O[d], 0, 0, 0);
+        }
+    }
+    if (!active) return;
+    const int tq = q0 + li;
+    if (a.lse && g == 0 && tq < T)
+        a.lse[((int64_t)b * gridDim.y + h) * T + tq] = (mrun + log2f(lrun)) * 0.69314718055994530942f;
+    if (tq < T) {
+        float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
+        const float inv = 1.0f / lrun;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            f4 v = O[d] * inv;
+            *(f4*)(op + 16 * d + 4 * g) = v;
         }
     }
 }
@@ -1276,8 +1433,8 @@ __global__ __launch_bounds__(256) void attention_lds_kernel(AttnArgs a) {
                     const f4 v0 = *(const f4*)kp, v1 = *(const f4*)(kp + 4);
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        kr[e][t] = key < T ? v0[t] * a.scale : 0.f;
-                        kr[e][4 + t] = key < T ? v1[t] * a.scale : 0.f;
+                        kr[e][t] = key < T ? v0[t] * kln2(a.scale) : 0.f;
+                        kr[e][4 + t] = key < T ? v1[t] * kln2(a.scale) : 0.f;
                     }
                 }
                 {   // V: channel ci, keys kmap(gg, 0..7)
@@ -1365,13 +1522,13 @@ __global__ __launch_bounds__(256) void attention_lds_kernel(AttnArgs a) {
             mx = fmaxf(mx, __shfl_xor(mx, 16));
             mx = fmaxf(mx, __shfl_xor(mx, 32));
             const float mnew = fmaxf(mrun, mx);
-            const float alpha = expf(mrun - mnew);
+            const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
             float p[8], ps = 0.f;
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    p[4 * u + r] = expf(st[u][r] - mnew);
+                    p[4 * u + r] = __builtin_amdgcn_exp2f(st[u][r] - mnew);
                     ps += p[4 * u + r];
                 }
             ps += __shfl_xor(ps, 16);
@@ -1397,7 +1554,8 @@ __global__ __launch_bounds__(256) void attention_lds_kernel(AttnArgs a) {
     }
     if (!active) return;
     const int tq = q0 + li;
-    if (a.lse && g == 0 && tq < T) a.lse[((int64_t)b * gridDim.y + h) * T + tq] = mrun + logf(lrun);
+    if (a.lse && g == 0 && tq < T)
+        a.lse[((int64_t)b * gridDim.y + h) * T + tq] = (mrun + log2f(lrun)) * 0.69314718055994530942f;
     if (tq < T) {
         float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
         const float inv = 1.0f / lrun;
@@ -1764,6 +1922,25 @@ void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* 
     hipLaunchKernelGGL(attn_kv_split_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, st, a, CH, heads, B,
                        kf, vf);
     check_launch("attn_kv_split_kernel");
+    // K4d (default; CFD_ATTN_DMA=0 restores K4s): fragments staged per workgroup
+    // by LDS-DMA, 8 waves (128 queries) per workgroup where T >= 512, else 4 (the
+    // choice changes no result: every query's arithmetic is the same)
+    static const int dma = env_int("CFD_ATTN_DMA", 1);
+    if (dma) {
+        const int w8 = a.T >= 512;
+        const dim3 grid((unsigned)ceil_div(a.T, w8 ? 128 : 64), heads, B);
+        const dim3 blk(w8 ? 512 : 256);
+        switch (CH * 2 + w8) {
+            case 64: hipLaunchKernelGGL((attention_dma_kernel<32, 4>), grid, blk, 0, st, a, kf, vf); break;
+            case 65: hipLaunchKernelGGL((attention_dma_kernel<32, 8>), grid, blk, 0, st, a, kf, vf); break;
+            case 128: hipLaunchKernelGGL((attention_dma_kernel<64, 4>), grid, blk, 0, st, a, kf, vf); break;
+            case 129: hipLaunchKernelGGL((attention_dma_kernel<64, 8>), grid, blk, 0, st, a, kf, vf); break;
+            case 256: hipLaunchKernelGGL((attention_dma_kernel<128, 4>), grid, blk, 0, st, a, kf, vf); break;
+            default: hipLaunchKernelGGL((attention_dma_kernel<128, 8>), grid, blk, 0, st, a, kf, vf); break;
+        }
+        check_launch("attention_dma_kernel");
+        return;
+    }
     // CFD_ATTN_QT=2: two query tiles per wave where that still leaves >= 256
     // workgroups (per sample: the choice must not depend on the batch).  Measured
     // slower (U-Net 4.48 -> 4.62 ms same-box: 181 registers halve the waves per

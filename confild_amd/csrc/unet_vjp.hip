@@ -17,6 +17,10 @@
 namespace cfd {
 
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+// e^x for the recomputed attention probabilities (x = S - lse <= ~0): one multiply
+// and v_exp_f32 instead of ocml's ~11-instruction expf; the rounding of x log2(e)
+// is 2^-24 relative to |x|, below the split-f16 forward's own S error
+__device__ __forceinline__ float exp_nat(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896340736f); }
 
 // Per-thread constants of a channel quad c0..c0+3 of sample b: forward scale /
 // shift, gamma, group mean / rstd (loaded once, not per pixel).
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         // lane (g, li): S[query li][key kb + 4g + r], dP likewise
         float ds[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ds[r] = expf(st[r] - lse) * (dpt[r] - dsum);
+        for (int r = 0; r < 4; ++r) ds[r] = exp_nat(st[r] - lse) * (dpt[r] - dsum);
         // dQ^T[d][query] += K^T[d][key] dS^T[key][query]
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -325,7 +329,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
             const f4 d4 = *(const f4*)(a.dd + row + qb + 4 * g);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                p[r] = expf(st[r] - l4[r]);
+                p[r] = exp_nat(st[r] - l4[r]);
                 ds[r] = p[r] * (dp[r] - d4[r]);
             }
         }
