@@ -432,8 +432,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     static_assert(AIT >= 1 && BIT >= 1 && TM >= 1, "tile too small for the wave count");
     // floats per LDS tile: fp32 BM*BK; bf16 half that; split two f16 tiles (hi, lo)
     constexpr int AFL = BF ? BM * BK / 2 : BM * BK, BFL = BF ? BN * BK / 2 : BN * BK;
-    __shared__ __attribute__((aligned(16))) float As[2][AFL];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BFL];
+    // one array: the epilogue (a.ldsepi) reuses all of it as a BM x BN fp32 tile
+    __shared__ __attribute__((aligned(16))) float smem_ab[2 * AFL + 2 * BFL];
+    float(*const As)[AFL] = (float(*)[AFL])smem_ab;
+    float(*const Bs)[BFL] = (float(*)[BFL])(smem_ab + 2 * AFL);
+    constexpr bool LDSEPI_FITS = !BF && BM * BN <= 2 * AFL + 2 * BFL;
     // buffer-addressed forward (a.bufaddr): source pixel of every (tap, tile row),
     // -1 for padding, built once per workgroup; the tile loads then cost one table
     // read, one 24-bit multiply-add and a select per row instead of the 64-bit
@@ -755,6 +758,47 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] *= a.acc_scale;
+    }
+    // LDS epilogue (a.ldsepi, Cout % 4 == 0): the accumulators go through LDS
+    // (every wave is past its last fragment read: the K loop ends on a barrier)
+    // so the stores -- and the residual / bias loads -- are float4 rows of BN
+    // channels instead of the 16x16 accumulator layout's 64-B column pieces.
+    // Columns XOR-swizzled by 16 ((row >> 2) & 3) so the four row groups of a
+    // write land in different banks.  Same values, same rounding.
+    if constexpr (LDSEPI_FITS) {
+        if (a.ldsepi) {
+            __syncthreads();
+            float* tile = smem_ab;
+            auto sw = [](int row, int col) { return row * BN + (col ^ (((row >> 2) & 3) << 4)); };
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        tile[sw(wm * WM + 16 * i + g4 + r, wn * WN + 16 * j + li)] = acc[i][j][r];
+            __syncthreads();
+            constexpr int NV = BM * BN / 4 / (64 * NW);
+            float* part = gridDim.z > 1 ? a.part + (int64_t)bz * a.M * a.Cout : nullptr;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int idx = tid + v * 64 * NW;
+                const int row = idx / (BN / 4), c4 = (idx - row * (BN / 4)) * 4;
+                const int m = m0 + row, n = n0 + c4;
+                if (m >= a.M || n >= a.Cout) continue;
+                f4 val = *(const f4*)&tile[sw(row, c4)];
+                const int64_t o = (int64_t)m * a.Cout + n;
+                if (part) {
+                    *(f4*)(part + o) = val;
+                    continue;
+                }
+                if (a.bias) val = val + *(const f4*)(a.bias + n);
+                if (a.emb) val = val + *(const f4*)(a.emb + (int64_t)(m / HWo) * a.emb_stride + n);
+                if (a.res) val = *(const f4*)(a.res + o) + val;
+                *(f4*)(a.out + o) = val;
+            }
+            return;
+        }
     }
     if (gridDim.z > 1) {
         float* part = a.part + (int64_t)bz * a.M * a.Cout;
@@ -1744,8 +1788,11 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // has >= 256 pixels at batch 8, 128x128 / 4 waves below (tools/convbench:
     // 1.04-1.11x / 1.17x the K1s tiles on the config-B shapes, same box)
     static const int kx = env_int("CFD_CONV_KX", 1);
+    // CFD_CONV_KX1 (development): K1x also for the 1x1 and stride-2 convolutions
+    static const int kx1 = env_int("CFD_CONV_KX1", 0);
+    const bool kx_shape = (a.ks == 3 && a.stride == 1) || (kx1 && !a.up && (a.ks == 1 || a.stride == 2));
     const int64_t srows = mn / ((int64_t)a.Hout * a.Wout) * a.Hin * a.Win;
-    if (kx && a.wbf && a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 &&
+    if (kx && a.wbf && a.wlo && !a.tmode && kx_shape && a.Cout >= 128 &&
         srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31)) {
         ConvPlan q;
         // K1h (halo tiles, conv_x.hip) where a 256-pixel block tiles the image
@@ -1754,7 +1801,7 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
         // the config-B 64^2/32^2 shapes, 1.04-1.17x at 16^2 with split-K 8);
         // split-K over the chunks, at least one chunk per split
         static const int kh = env_int("CFD_CONV_KH", 1);
-        if (kh && conv_h_tw(a) > 0) {
+        if (kh && a.ks == 3 && a.stride == 1 && conv_h_tw(a) > 0) {
             q.kx = 20;
             q.bm = 256;
             q.bn = 128;
@@ -1824,7 +1871,10 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     static const int xcd = env_int("CFD_CONV_XCD", 1);
     static const int korder = env_int("CFD_CONV_KORDER", 0);
     static const int bufaddr = env_int("CFD_CONV_BUFADDR", 1);
+    static const int ldsepi = env_int("CFD_CONV_LDSEPI", 1);
     ConvArgs b = a;
+    // float4 rows need Cout % 4 == 0 and 16-B aligned bias / emb / res / out rows
+    b.ldsepi = ldsepi && a.Cout % 4 == 0 && a.emb_stride % 4 == 0;
     // 1: splits-fastest XCD order; 2: m-fastest (weight-sharing) order; 3: order 2 where
     // the per-sample image has <= 256 pixels (the small-M levels), else 1
     b.xcd = xcd == 3 ? ((int64_t)a.Hout * a.Wout <= 256 ? 2 : 1) : xcd < 0 || xcd > 2 ? 1 : xcd;

@@ -53,6 +53,7 @@ struct ConvArgs {
     int xcd;             // XCD-contiguous workgroup order (set by launch_conv; CFD_CONV_XCD=0: off)
     int korder;          // K tile order: 0 (tap, channel chunk), 1 (channel chunk, tap) (set by launch_conv)
     int bufaddr;         // 32-bit buffer addressing of the operands (set by launch_conv where it fits)
+    int ldsepi;          // K1s: epilogue through LDS, float4 rows (set by launch_conv; CFD_CONV_LDSEPI=0: off)
     int* nonfinite;      // conv_out only: set to 1 when an output is not finite (range guard), or null
 };
 
