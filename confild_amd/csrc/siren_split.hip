@@ -127,7 +127,7 @@ __device__ __forceinline__ float sin_hw(float x) {
     return __builtin_amdgcn_sinf(r * 0.159154943091895335768f);
 }
 
-// sin(x) with the reduction in revolutions (the split32 default, CFD_SIREN_HWSIN=2):
+// sin(x) with the reduction in revolutions (CFD_SIREN_HWSIN=2; the split32 default before HWSIN 4):
 // q = rint(x / 2pi), r = x C_hi - q + x C_lo with 1/2pi = C_hi + C_lo (fma: x C_hi - q
 // is exact before its one rounding), then v_sin_f32 on r.  4 VALU + one
 // transcendental against sin_hw's 7; two roundings of |r| <= 1/2 (2^-26 rev each)
