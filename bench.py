@@ -204,6 +204,129 @@ def step_B(o, dev, seed, start, count, ev=None):
 
 
 # ---------------------------------------------------------------------------
+# configs A and E (BASELINE.json configs[0] / configs[4]): the same sample ->
+# de-normalise -> decode chain at their own shapes, samples sharded like B (weak)
+#   A: Case1 uncond, U-Net 32^2 (channel_mult 1,2,3,4), DDIM-50, SIREN(2,32,3,10,128)
+#      on 1000 coordinates, B = 1 per GPU (the reference's CPU-runnable case)
+#   E: Case3, U-Net 128^2 with bf16 convolution operands (fp32 accumulate), DDPM
+#      1000 steps, SIREN(2,128,2,17,256) on a 256^2 lattice, B = 8 per GPU (64 on 8)
+# ---------------------------------------------------------------------------
+UNCOND_CFG = {
+    "A": dict(size=32, channel_mult="1,2,3,4", respacing="ddim50", ddim=True, batch=1,
+              siren=dict(d=2, L=32, c=3, nh=10, H=128), coords=1000, unet="split_f16",
+              gflops=19.23),
+    "E": dict(size=128, channel_mult="", respacing="", ddim=False, batch=8,
+              siren=dict(d=2, L=128, c=2, nh=17, H=256), coords=256 * 256, unet="bf16",
+              gflops=140.75),
+}
+
+
+def main_uncond(args, rank, world, dev):
+    from confild_amd import _lib
+    from confild_amd import dist as cdist
+    from confild_amd import synth
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    from confild_amd.normalize import Normalizer_ts
+    from confild_amd.script_util import create_gaussian_diffusion, create_model
+    c = UNCOND_CFG[args.config]
+    Sz, sc = c["size"], c["siren"]
+    model = create_model(image_size=Sz, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                         attention_resolutions="32,16,8", channel_mult=c["channel_mult"])
+    nf = SIRENAutodecoder_film(sc["d"], sc["L"], sc["c"], sc["nh"], sc["H"])
+    if rank == 0:
+        sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in model.state_dict().items()})
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        nf.load_state_dict({k: torch.from_numpy(v) for k, v in
+                            synth.siren_state_dict(1234, sc["d"], sc["L"], sc["c"], sc["nh"], sc["H"]).items()})
+    model.to(dev)
+    nf.to(dev)
+    cdist.broadcast_module(model)
+    cdist.broadcast_module(nf)
+    model.set_compute(c["unet"] if args.unet_compute == "split_f16" else args.unet_compute)
+    nf.set_compute(args.siren_compute)
+    diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=c["respacing"])
+    nsteps = diff.num_timesteps
+    if args.config == "E":
+        ax = torch.linspace(0, 1, 256)
+        coords = torch.stack(torch.meshgrid(ax, ax, indexing="ij"), -1).reshape(-1, 2).to(dev)
+    else:
+        coords = torch.from_numpy(synth.uniform(7, "A/coords", (c["coords"], 2), 0.0, 1.0)).to(dev)
+    N = coords.shape[0]
+    xn = Normalizer_ts(params=(torch.ones(1, 2, device=dev), torch.zeros(1, 2, device=dev)), method="-11", dim=0)
+    ymax = torch.from_numpy(synth.uniform(9, "ymax", (1, N, sc["c"]), 0.5, 2.0)).to(dev)
+    ymin = -torch.from_numpy(synth.uniform(9, "ymin", (1, N, sc["c"]), 0.5, 2.0)).to(dev)
+    yn = Normalizer_ts(params=(ymax, ymin), method="-11", dim=0)
+    vmax, vmin = torch.full((1,), 1.5, device=dev), torch.full((1,), -1.5, device=dev)
+    batch = args.batch or c["batch"]
+    glob = batch * world
+    start = rank * batch
+    sizes = [batch * Sz] * world
+
+    def one(k, ev=None):
+        if ev is not None:
+            ev[0].record()
+        loop = diff.ddim_sample_loop if c["ddim"] else diff.p_sample_loop
+        lat = loop(model, (batch, 1, Sz, Sz), seed=10 ** 6 + k, sample_offset=start)[:, 0]
+        den = torch.empty_like(lat)
+        _lib.check(_lib.load().cfd_latent_denorm(_lib.ptr(lat), _lib.ptr(den), lat.numel(), _lib.ptr(vmax),
+                                                 _lib.ptr(vmin), 1, _lib.stream_of(dev)), "denorm")
+        if ev is not None:
+            ev[1].record()
+        f = nf.decode(coords, den.reshape(batch * Sz, 1, Sz), xn, yn)
+        if ev is not None:
+            ev[2].record()
+        return gather_to_root(f, 0, sizes, world) if world > 1 and not args.no_gather else f
+
+    for w in range(args.warmup):
+        one(-1 - w)
+    barrier(dev, world)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        out = one(k, evs[k])
+    barrier(dev, world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev, world)
+    unet_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in evs]))
+    dec_ms = float(np.mean([ev[1].elapsed_time(ev[2]) for ev in evs]))
+    model.check_finite(dev)
+    if rank == 0:
+        assert torch.isfinite(out).all().item(), "non-finite output"
+        mode = nf.compute_mode(dev)
+        kname, peak, peak_basis, _ = ROOFLINE[mode]
+        flops = batch * Sz * N * siren_flops_per_pair(**sc)
+        uf = batch * c["gflops"] * 1e9 * nsteps
+        ua = uf / (unet_ms / 1e3) / 1e12
+        upeak = F16_PEAK_TFLOPS if model.compute == "bf16" else F16_PEAK_TFLOPS / 3
+        rec = {"metric": METRIC.replace("256-step", f"{nsteps}-step").replace("Case4", "Case1" if args.config == "A"
+                                                                               else "Case3"),
+               "value": glob * args.steps / elapsed, "unit": "fields/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if model.compute == "bf16" else "f32",
+               "data": "synthetic (seeded weights and inputs; no checkpoints)",
+               "compute": {"unet": model.compute, "cnf_decoder": mode},
+               "config": {"workload": (f"config {args.config}: U-Net {Sz}x{Sz} (channel_mult "
+                                       f"{c['channel_mult'] or 'default'}), {'DDIM-50' if c['ddim'] else 'DDPM'} "
+                                       f"{nsteps} steps, {batch}/GPU, CNF SIREN({sc['d']},{sc['L']},{sc['c']},"
+                                       f"{sc['nh']},{sc['H']}) decode of {Sz} latent rows per sample on {N} coords"),
+                          "global_batch": glob, "seq_len": Sz, "parallelism": f"dp{world} ({batch} samples per GPU)"},
+               "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)",
+                            "achieved": flops / (dec_ms / 1e3) / 1e12, "peak": peak, "peak_basis": peak_basis,
+                            "unit": "TFLOP/s", "frac": flops / (dec_ms / 1e3) / 1e12 / peak, "traffic": None,
+                            "flops_per_launch": flops, "launch_ms": dec_ms},
+               "roofline_unet": {"bound": "mfma", "kernel": f"U-Net forward x {nsteps} steps (all kernels + step)",
+                                 "achieved": ua, "peak": upeak,
+                                 "peak_basis": "bf16 dense MFMA peak" if model.compute == "bf16" else
+                                 "f16 dense MFMA peak / 3 (split-f16 convolutions)",
+                                 "unit": "TFLOP/s", "frac": ua / upeak, "flops": uf, "ms": unet_ms,
+                                 "ms_per_forward": unet_ms / nsteps},
+               "cpu_baseline": None}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
 # config C: coordinate-sharded CNF-only decode
 # ---------------------------------------------------------------------------
 def setup_C(dev, rank, world, siren_compute):
@@ -419,10 +542,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=["B", "C", "D", "Case4"], default="B")
+    ap.add_argument("--config", choices=["A", "B", "C", "D", "E", "Case4"], default="B")
     ap.add_argument("--dps-steps", type=int, default=0,
                     help="D / Case4: time this many reverse steps of the loop (0: the whole loop)")
-    ap.add_argument("--batch", type=int, default=0, help="D / Case4: chains per GPU (0: the config's)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="A / E: samples per GPU; D / Case4: chains per GPU (0: the config's)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-gather", action="store_true", help="keep decoded fields on their ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -436,6 +560,8 @@ def main():
 
     if args.config in ("D", "Case4"):
         return main_dps(args, rank, world, dev)
+    if args.config in ("A", "E"):
+        return main_uncond(args, rank, world, dev)
     if args.config == "B":
         o = setup_B(dev, rank, world, args.siren_compute, args.unet_compute)
         nf = o["nf"]

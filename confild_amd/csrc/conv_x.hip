@@ -367,9 +367,13 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // stores, wrong results) reach 1.0-1.1 / 1.1 / 1.05 / 1.2 / all four 1.3x --
 // the MFMA chain alone runs at ~430 TF fp32-equivalent on random data at the
 // clock the chip holds under it, ~0.52 of the 2.4 GHz split-f16 peak.
-template <int BM, int TW, int KG = 1>
+// BF (config E, K1hb): bf16 operands -- the halo rounded to bf16 (RNE) as it is
+// staged, weights from the bf16 arena (a.wbf, a.wlo null) -- one
+// v_mfma_f32_32x32x16_bf16 per product, one halo plane and one weight plane.
+template <int BM, int TW, int KG = 1, bool BF = false>
 __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     constexpr int BN = 128, WGM = BM / 64, NTG = 64 * WGM * 2;   // threads per K group (the workgroup: NTG * KG)
+    constexpr int PL = BF ? 1 : 2;                                 // operand planes: bf16, or f16 hi + lo
     // halo row stride HW2: TW + 2 columns, padded to a multiple of 4 where a
     // 32-pixel fragment block spans two tile rows (TW = 16), so the second row's
     // lanes keep the swizzle's bank pattern (PMC: 0.25 LDS bank-conflict rate
@@ -378,9 +382,9 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     constexpr int TR = BM / TW, NPX = (TR + 2) * HW2;
     constexpr int HPLANE = NPX * 64;                  // one f16 plane of the halo (64 B per pixel)
     constexpr int HIT = (NPX * 8 + NTG - 1) / NTG;    // 16-B halo pieces per thread
-    constexpr int BPLANE = BN * 64, BSTAGE = 2 * BPLANE;
+    constexpr int BPLANE = BN * 64, BSTAGE = PL * BPLANE;
     constexpr int BIT = BN * 4 / NTG;                 // 16-B weight pieces per thread and plane
-    constexpr int GBYTES = 2 * HPLANE + 2 * BSTAGE;   // one group's halo + weight ring
+    constexpr int GBYTES = PL * HPLANE + 2 * BSTAGE;  // one group's halo + weight ring
     static_assert(BM % TW == 0 && BIT >= 1, "tile");
     constexpr int RED = (KG - 1) * WGM * 2 * 4 * 16 * 64 * 4;   // parked sums of groups 1..
     __shared__ __attribute__((aligned(16))) char lds[KG * GBYTES > RED ? KG * GBYTES : RED];
@@ -391,7 +395,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     const int wm = wrem >> 1, wn = wrem & 1;
     const int gt = tid - kg * NTG;   // thread index within the group
     char* const halo = lds + kg * GBYTES;
-    char* const ring = halo + 2 * HPLANE;
+    char* const ring = halo + PL * HPLANE;
     int bx, by, bz;
     xcd_tile(a.xcd, bx, by, bz);
     const int n0 = by * BN;
@@ -470,11 +474,15 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
         for (int it = 0; it < HIT; ++it) {
             const int e = gt + it * NTG;
             if (e < NPX * 8) {
-                uint2 hv, lv;
-                split4_mix_x(rh[it], hv, lv);
                 const int off = xswz(e >> 3, kq >> 1) + (kq & 1) * 8;
-                *(uint2*)(halo + off) = hv;
-                *(uint2*)(halo + HPLANE + off) = lv;
+                if constexpr (BF) {
+                    *(bf16x4*)(halo + off) = __builtin_convertvector(rh[it], bf16x4);
+                } else {
+                    uint2 hv, lv;
+                    split4_mix_x(rh[it], hv, lv);
+                    *(uint2*)(halo + off) = hv;
+                    *(uint2*)(halo + HPLANE + off) = lv;
+                }
             }
         }
     };
@@ -486,7 +494,8 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
             rbh[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwh, bvoff[it], soff, 0));
-            rbl[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwl, bvoff[it], soff, 0));
+            if constexpr (!BF)
+                rbl[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwl, bvoff[it], soff, 0));
         }
     };
     auto store_w = [&](int stage, const u4 (&rbh)[BIT], const u4 (&rbl)[BIT]) {
@@ -495,7 +504,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
         for (int it = 0; it < BIT; ++it) {
             const int off = xswz((gt >> 2) + it * (NTG / 4), bq);
             *(u4*)(base + off) = rbh[it];
-            *(u4*)(base + BPLANE + off) = rbl[it];
+            if constexpr (!BF) *(u4*)(base + BPLANE + off) = rbl[it];
         }
     };
 
@@ -533,6 +542,19 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const int ch = 2 * s2 + hsel;
+                if constexpr (BF) {
+                    bf16x8 fa[2], fb[2];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) fa[i] = *(const bf16x8*)(halo + xswz(hb[i] + tofs, ch));
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) fb[j] = *(const bf16x8*)(wb + xswz(brow0 + 32 * j, ch));
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                    continue;
+                }
                 h8v fah[2], fal[2], fbh[2], fbl[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
@@ -617,10 +639,12 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
         }
     }
 
+    if constexpr (!BF) {   // undo the split weights' power-of-two scale (exact)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] *= a.acc_scale;
+            for (int j = 0; j < 2; ++j) acc[i][j] *= a.acc_scale;
+    }
     const int n_base = n0 + wn * 64 + l32;
     const int p_base = wm * 64 + 4 * hsel;   // tile position of acc element 0 of block 0
     auto pix_of = [&](int p) { return mrow0 + (int64_t)(p / TW) * W + (p % TW); };
@@ -922,7 +946,8 @@ int conv_h_tw(const ConvArgs& a) {
 }
 
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
-    CFD_REQUIRE(a.wbf && a.wlo && !a.tmode, CFD_ESTATE, "conv_x: split-f16 forward only");
+    CFD_REQUIRE(a.wbf && (a.wlo || variant == 22) && !a.tmode, CFD_ESTATE,
+                "conv_x: split-f16 forward only (variant 22: bf16)");
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_x needs channels % 32 == 0");
     CFD_REQUIRE(splits == 1 || a.part, CFD_ESTATE, "split-K needs a partial buffer");
     {   // K1x / K1y: 32-bit buffer offsets, 24-bit pixel indices
@@ -934,6 +959,16 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
     auto grid = [&](int bm, int bn) {
         return dim3((unsigned)ceil_div(a.M, bm), (unsigned)ceil_div(a.Cout, bn), splits);
     };
+    if (variant == 22) {   // K1hb: bf16 operands, 256-pixel blocks
+        const int tw = conv_h_tw(a);
+        CFD_REQUIRE(tw > 0 && !a.wlo, CFD_ESHAPE, "conv_h bf16: 3x3 stride-1 with a 16/32/64-divisible width");
+        const dim3 g = grid(256, 128);
+        if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true>), g, dim3(512), 0, st, a);
+        else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, true>), g, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, true>), g, dim3(512), 0, st, a);
+        check_launch("conv_h_kernel");
+        return splits;
+    }
     if (variant == 20 || variant == 21) {   // K1h: 20 = 256-pixel blocks; 21 = 128-pixel blocks in 2 K groups
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0 && (variant == 20 || (a.Hout * a.Wout) % 128 == 0), CFD_ESHAPE,

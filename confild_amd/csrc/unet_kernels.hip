@@ -1792,6 +1792,23 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     static const int kx1 = env_int("CFD_CONV_KX1", 0);
     const bool kx_shape = (a.ks == 3 && a.stride == 1) || (kx1 && !a.up && (a.ks == 1 || a.stride == 2));
     const int64_t srows = mn / ((int64_t)a.Hout * a.Wout) * a.Hin * a.Win;
+    // K1hb (conv_x.hip): the bf16-operand convolutions (config E) on the halo tiles
+    static const int khb = env_int("CFD_CONV_KHB", 1);
+    if (khb && kx && a.wbf && !a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 &&
+        srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31) &&
+        conv_h_tw(a) > 0) {
+        ConvPlan q;
+        q.kx = 22;
+        q.bm = 256;
+        q.bn = 128;
+        q.nw = 8;
+        const int64_t t = ceil_div(mn, 256) * ceil_div(a.Cout, 128);
+        const int nch = a.Ctot / 32;
+        q.splits = 1;
+        while (t * q.splits < 256 && q.splits * 2 <= nch && q.splits < 16) q.splits *= 2;
+        while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
+        return q;
+    }
     if (kx && a.wbf && a.wlo && !a.tmode && kx_shape && a.Cout >= 128 &&
         srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31)) {
         ConvPlan q;
