@@ -56,10 +56,13 @@ C_LATENTS = 256
 FMA_PEAK_TFLOPS = 157.3    # MI355X fp32 matrix peak (MI355X_MICROARCH.md chip table)
 F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16/bf16 matrix peak (same table; no sparsity)
 # measured: every SIMD issuing v_mfma_f32_32x32x16_f16 back to back on random
-# operands holds ~1.62 GHz, 1693.5 TFLOP/s f16 (zero operands: 2477 at 2.36 GHz);
-# tools/mfma_peak.cpp, profiles/r02_mfma_peak.json.  /3 = the ceiling a split-f16
-# kernel can reach on real data at the clock the chip holds
-F16_SUSTAINED_TFLOPS = 1693.5
+# operands: 1693.5 TFLOP/s f16 at two waves per SIMD (tools/mfma_peak.cpp,
+# profiles/r02_mfma_peak.json; zero operands: 2477 at 2.36 GHz) and up to 1809.9
+# at one wave per SIMD, one dependent chain or several (tools/mfma_chain.cpp,
+# profiles/r02_mfma_chain.json) -- the higher, the decoder's configuration, is
+# the ceiling used.  /3 = what a split-f16 kernel can reach on real data at the
+# clock the chip holds
+F16_SUSTAINED_TFLOPS = 1809.9
 UNET_FLOPS_PER_SAMPLE = 68.61e9   # config-B U-Net forward, 2*MAC of conv/bmm/addmm (FlopCounter)
 METRIC = "generated fields/sec (256-step sample + CNF decode), Case4 latent, 1/2/4/8 GPU"
 
@@ -653,7 +656,7 @@ def main():
                          **({"peak_sustained": F16_SUSTAINED_TFLOPS / 3,
                              "frac_sustained": achieved / (F16_SUSTAINED_TFLOPS / 3),
                              "sustained_basis": "measured back-to-back f16 MFMA on random operands / 3 "
-                                                "(tools/mfma_peak.cpp, profiles/r02_mfma_peak.json)"}
+                                                "(tools/mfma_chain.cpp, profiles/r02_mfma_chain.json)"}
                             if mode == "split_f16" else {})},
             "cpu_baseline": cpu,
         }
