@@ -1780,6 +1780,12 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     p.splits = 1;
     while (tiles(p.bm) * wg_per_tile * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16)
         p.splits *= 2;
+    // 1x1 convolutions (qkv, proj_out, skip) with >= 128 tiles: no split-K.  Their
+    // K is short (256-640), so a split only adds partial slabs and a reduction pass
+    // (convbench, reduction included: 1.09-1.72x unsplit on the config-B shapes
+    // with 128-256 tiles, 0.5-0.8x below; CFD_CONV_1X1_SPLIT=1 restores the target)
+    static const int split1x1 = env_int("CFD_CONV_1X1_SPLIT", 0);
+    if (!split1x1 && a.ks == 1 && !a.tmode && tiles(p.bm) >= 128) p.splits = 1;
     // memory guard, on the nominal shape too: part_cap_floats is the slab per 8
     // samples (the caller sizes the real slab as ceil(B/8) of these)
     while (p.splits > 1 && (size_t)p.splits * mn * a.Cout > part_cap_floats) p.splits /= 2;
