@@ -462,7 +462,8 @@ __device__ __forceinline__ void split_chunk(const float (&x)[16], int e, Frag& h
 }
 
 // EXP (timing experiments only, wrong results): bit 0 no weight streaming / barrier,
-// bit 1 no sine (x = scaled accumulator), bit 2 A-fragment prefetch two steps ahead
+// bit 1 no sine (x = scaled accumulator), bit 2 no per-step A-fragment LDS reads
+// (every step reuses the block's first fragments)
 template <int NB2, int EXP = 0, int HWSIN = 0>
 __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
     constexpr int NK = 2 * NB2;    // 16-deep K chunks per layer
@@ -597,7 +598,7 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
             static_for<NK>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 h8 FH1 = FH, FL1 = FL;
-                if constexpr (k + 1 < NK) {
+                if constexpr (k + 1 < NK && !(EXP & 4)) {
                     FH1 = *(const h8*)(wb + (k + 1) * 512 + lane * 4);
                     FL1 = *(const h8*)(wb + (k + 1) * 512 + 256 + lane * 4);
                 }
@@ -780,7 +781,12 @@ void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
             case 64: return hw == 3 ? launch_split32<2, 0, 3>(a, b, st) : launch_split32<2, 0, 4>(a, b, st);
             case 128: return hw == 3 ? launch_split32<4, 0, 3>(a, b, st) : launch_split32<4, 0, 4>(a, b, st);
             case 256: return hw == 3 ? launch_split32<8, 0, 3>(a, b, st) : launch_split32<8, 0, 4>(a, b, st);
-            case 384: return hw == 3 ? launch_split32<12, 0, 3>(a, b, st) : launch_split32<12, 0, 4>(a, b, st);
+            case 384: {
+                static const int exp = env_int("CFD_SIREN_EXP", 0, 0, 4);
+                if (hw == 4 && exp == 4) return launch_split32<12, 4, 4>(a, b, st);   // timing experiment
+                if (hw == 4 && exp == 1) return launch_split32<12, 1, 4>(a, b, st);   // timing experiment
+                return hw == 3 ? launch_split32<12, 0, 3>(a, b, st) : launch_split32<12, 0, 4>(a, b, st);
+            }
             default: break;
         }
     }
@@ -798,11 +804,12 @@ void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
         case 128: return launch_split32<4>(a, b, st);
         case 256: return launch_split32<8>(a, b, st);
         case 384: {
-            static const int exp = env_int("CFD_SIREN_EXP", 0, 0, 3);
+            static const int exp = env_int("CFD_SIREN_EXP", 0, 0, 4);
             switch (exp) {
                 case 1: return launch_split32<12, 1>(a, b, st);
                 case 2: return launch_split32<12, 2>(a, b, st);
                 case 3: return launch_split32<12, 3>(a, b, st);
+                case 4: return launch_split32<12, 4>(a, b, st);
                 default: return launch_split32<12>(a, b, st);
             }
         }
