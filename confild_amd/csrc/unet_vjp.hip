@@ -16,7 +16,9 @@
 
 namespace cfd {
 
-__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float sigmoid_f(float x) {   // the forward's SiLU form (unet_kernels.hip silu_f)
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896340736f));
+}
 // e^x for the recomputed attention probabilities (x = S - lse <= ~0): one multiply
 // and v_exp_f32 instead of ocml's ~11-instruction expf; the rounding of x log2(e)
 // is 2^-24 relative to |x|, below the split-f16 forward's own S error
