@@ -12,6 +12,7 @@
 #include <string>
 
 #include "common.hpp"
+#include "sampler.hpp"
 
 namespace cfd {
 
@@ -77,6 +78,7 @@ struct StepArgs {
     int64_t total;       // B * n
     uint64_t seed, counter, goff;  // goff: Philox group offset (= element offset / 4)
     int kind, clip;
+    const SamplerCtl* ctl;         // native loop: (seed, counter, goff) from device memory, or null
 };
 
 __global__ void step_kernel(StepArgs a) {
@@ -88,6 +90,8 @@ __global__ void step_kernel(StepArgs a) {
     if (a.noise) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) z[j] = (base + j < a.total) ? a.noise[base + j] : 0.f;
+    } else if (a.ctl) {
+        Philox::normal4(a.ctl->seed, a.ctl->counter, a.ctl->goff + (uint64_t)grp, z);
     } else {
         Philox::normal4(a.seed, a.counter, a.goff + (uint64_t)grp, z);
     }
@@ -192,6 +196,32 @@ __global__ void dps_update_kernel(const float* __restrict__ sample, const float*
     x_out[i] = sample[i] - (g_direct[i] + g_unet[i]) * scale;
 }
 
+// native loop bookkeeping (one workgroup): the step's timesteps from the
+// host-built sequences, and the step counter for the Philox stream
+__global__ void sampler_advance_kernel(SamplerCtl* ctl, const int64_t* __restrict__ tidx_seq,
+                                       const int64_t* __restrict__ tmodel_seq, int64_t* __restrict__ t_idx,
+                                       int64_t* __restrict__ t_model, int B) {
+    const uint64_t k = ctl->k;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        t_idx[b] = tidx_seq[k];
+        t_model[b] = tmodel_seq[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ctl->counter = k;
+        ctl->k = k + 1;
+    }
+}
+
+__global__ void sampler_set_kernel(SamplerCtl* ctl, uint64_t k, uint64_t seed, uint64_t goff) {
+    if (threadIdx.x == 0) {
+        ctl->k = k;
+        ctl->counter = k;
+        ctl->seed = seed;
+        ctl->goff = goff;
+    }
+}
+
 }  // namespace cfd
 
 struct cfd_sched {
@@ -199,6 +229,30 @@ struct cfd_sched {
     int n_t = 0;
     int device = 0;
 };
+
+namespace cfd {
+const float* sched_coefs(const cfd_sched* s) { return s->coefs; }
+int sched_nt(const cfd_sched* s) { return s->n_t; }
+
+void launch_sampler_advance(SamplerCtl* ctl, const int64_t* tidx_seq, const int64_t* tmodel_seq, int64_t* t_idx,
+                            int64_t* t_model, int B, hipStream_t st) {
+    hipLaunchKernelGGL(sampler_advance_kernel, dim3(1), dim3(64), 0, st, ctl, tidx_seq, tmodel_seq, t_idx, t_model, B);
+    check_launch("sampler_advance_kernel");
+}
+
+void launch_sampler_set(SamplerCtl* ctl, uint64_t k, uint64_t seed, uint64_t goff, hipStream_t st) {
+    hipLaunchKernelGGL(sampler_set_kernel, dim3(1), dim3(64), 0, st, ctl, k, seed, goff);
+    check_launch("sampler_set_kernel");
+}
+
+void launch_sched_step_ctl(const cfd_sched* s, int kind, int clip, float* x, const float* eps, const int64_t* t,
+                           const SamplerCtl* ctl, int64_t n_per_sample, int B, hipStream_t st) {
+    StepArgs a{s->coefs, x, eps, t, nullptr, x, nullptr, n_per_sample, n_per_sample * B, 0, 0, 0, kind, clip, ctl};
+    const int64_t groups = ceil_div(a.total, 4);
+    hipLaunchKernelGGL(step_kernel, dim3((unsigned)ceil_div(groups, 256)), dim3(256), 0, st, a);
+    check_launch("step_kernel");
+}
+}  // namespace cfd
 
 extern "C" int cfd_sched_create(const float* host_coefs, int n_t, int device, cfd_sched** out) {
     return cfd::guard([&] {
@@ -228,7 +282,7 @@ extern "C" int cfd_sched_step(const cfd_sched* s, int kind, int clip, const floa
         CFD_REQUIRE(kind == CFD_STEP_DDPM || kind == CFD_STEP_DDIM, CFD_EARG, "unknown step kind");
         CFD_REQUIRE(n_per_sample > 0 && B > 0, CFD_EARG, "empty step");
         cfd::StepArgs a{s->coefs, x, eps, t, noise, x_out, xstart_out, n_per_sample, n_per_sample * B,
-                        seed, counter, offset / 4, kind, clip};
+                        seed, counter, offset / 4, kind, clip, nullptr};
         const int64_t groups = cfd::ceil_div(a.total, 4);
         hipLaunchKernelGGL(cfd::step_kernel, dim3((unsigned)cfd::ceil_div(groups, 256)), dim3(256), 0,
                            (hipStream_t)stream, a);

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "sampler.hpp"
 #include "unet_kernels.hpp"
 
 namespace cfd {
@@ -74,6 +75,9 @@ struct cfd_unet {
     uint16_t* arena_tlo = nullptr;
     int compute = CFD_COMPUTE_SPLIT_F16;
     int* nonfinite = nullptr;  // range guard flag: set by the last convolution on a non-finite eps
+    mutable std::map<int, size_t> ws_cache;  // workspace bytes per B (the dry walk is host work)
+    uint64_t version = 0;   // bumped by every set_param / set_compute: launch arguments (weight
+                            // scales, kernel choice) captured into a graph are stale after it
 };
 
 namespace {
@@ -1015,6 +1019,7 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
             CFD_HIP(hipMemcpy(h->arena_tlo + p.toffset, tlo.data(), pk.size() * 2, hipMemcpyHostToDevice));
         }
         p.set = true;
+        ++h->version;
     });
 }
 
@@ -1023,6 +1028,7 @@ extern "C" int cfd_unet_set_compute(cfd_unet* h, int compute) {
         CFD_REQUIRE(h, CFD_EARG, "null handle");
         CFD_REQUIRE(compute == CFD_COMPUTE_F32 || compute == CFD_COMPUTE_BF16 || compute == CFD_COMPUTE_SPLIT_F16,
                     CFD_EARG, "unknown compute mode");
+        if (h->compute != compute) ++h->version;
         h->compute = compute;
     });
 }
@@ -1042,12 +1048,33 @@ extern "C" int cfd_unet_ready(const cfd_unet* h) {
     });
 }
 
+namespace cfd {
+size_t unet_ws_bytes(const cfd_unet* h, int B) {
+    auto it = h->ws_cache.find(B);
+    if (it != h->ws_cache.end()) return it->second;
+    Workspace ws{nullptr, 0, true};
+    run(h, nullptr, nullptr, nullptr, B, ws, nullptr);
+    h->ws_cache[B] = ws.off + 256;
+    return ws.off + 256;
+}
+void unet_check_ready(const cfd_unet* h) {
+    for (const auto& p : h->params) CFD_REQUIRE(p.set, CFD_ESTATE, "U-Net parameter not set: " + p.key);
+}
+int unet_compute(const cfd_unet* h) { return h->compute; }
+uint64_t unet_version(const cfd_unet* h) { return h->version; }
+int unet_device(const cfd_unet* h) { return h->device; }
+int* unet_nonfinite(const cfd_unet* h) { return h->nonfinite; }
+void unet_forward_raw(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B, void* workspace,
+                      hipStream_t st) {
+    Workspace ws{(char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255)), 0, false};
+    run(h, x, t, eps, B, ws, st);
+}
+}  // namespace cfd
+
 extern "C" int cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes) {
     return cfd::guard([&] {
         CFD_REQUIRE(h && bytes && B > 0, CFD_EARG, "bad argument");
-        Workspace ws{nullptr, 0, true};
-        run(h, nullptr, nullptr, nullptr, B, ws, nullptr);
-        *bytes = ws.off + 256;
+        *bytes = cfd::unet_ws_bytes(h, B);
     });
 }
 
@@ -1056,12 +1083,9 @@ extern "C" int cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, f
     return cfd::guard([&] {
         CFD_REQUIRE(h && x && t && eps && workspace, CFD_EARG, "null argument");
         CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
-        for (const auto& p : h->params) CFD_REQUIRE(p.set, CFD_ESTATE, "U-Net parameter not set: " + p.key);
-        size_t need = 0;
-        cfd_unet_workspace_bytes(h, B, &need);
-        CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        Workspace ws{(char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255)), 0, false};
-        run(h, x, t, eps, B, ws, (hipStream_t)stream);
+        cfd::unet_check_ready(h);
+        CFD_REQUIRE(ws_bytes >= cfd::unet_ws_bytes(h, B), CFD_EARG, "workspace too small");
+        cfd::unet_forward_raw(h, x, t, eps, B, workspace, (hipStream_t)stream);
     });
 }
 

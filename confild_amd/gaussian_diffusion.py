@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes as C
 import enum
 import math
+import os
 
 import numpy as np
 import torch
@@ -106,6 +107,40 @@ class _Sched:
             pass
 
 
+class _NativeLoop:
+    """One cfd_sampler handle: the whole reverse loop on the device, one captured
+    HIP graph per `unroll` steps (csrc/sampler.hip).  Keeps the U-Net handle's
+    owner and the coefficient table alive for its lifetime."""
+
+    def __init__(self, model, sched, handle, kind, clip, B, n_per_sample, tidx, tmodel, graph, unroll):
+        lib = _lib.lib()
+        self.model, self.sched = model, sched
+        ti = np.ascontiguousarray(tidx, dtype=np.int64)
+        tm = np.ascontiguousarray(tmodel, dtype=np.int64)
+        self.handle = C.c_void_p()
+        _lib.check(lib.cfd_sampler_create(handle, sched.handle, kind, 1 if clip else 0, B, n_per_sample, len(ti),
+                                          ti.ctypes.data_as(C.c_void_p), tm.ctypes.data_as(C.c_void_p),
+                                          1 if graph else 0, unroll, C.byref(self.handle)), "cfd_sampler_create")
+
+    def run(self, x_in, x_out, k0, k1, seed, offset, device):
+        _lib.check(_lib.load().cfd_sampler_run(self.handle, _lib.ptr(x_in), _lib.ptr(x_out), k0, k1, seed, offset,
+                                               _lib.stream_of(device)), "cfd_sampler_run")
+
+    def __del__(self):
+        try:
+            _lib.load().cfd_sampler_destroy(self.handle)
+        except Exception:
+            pass
+
+
+# Native loop mode (CFD_SAMPLER): 2 = captured HIP graph (default), 1 = native
+# host loop without a graph, 0 = the Python per-step loop
+NATIVE_MODE = int(os.environ.get("CFD_SAMPLER", "2"))
+GRAPH_UNROLL = int(os.environ.get("CFD_SAMPLER_UNROLL", "4"))
+# the split-f16 range guard is read every RANGE_CHECK_EVERY steps (one stream sync each)
+RANGE_CHECK_EVERY = 64
+
+
 class GaussianDiffusion:
     """Same constructor and sampling API as the reference GaussianDiffusion (:88-169)."""
 
@@ -134,6 +169,11 @@ class GaussianDiffusion:
         self.posterior_mean_coef1 = betas * np.sqrt(self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
         self.posterior_mean_coef2 = (1.0 - self.alphas_cumprod_prev) * np.sqrt(alphas) / (1.0 - self.alphas_cumprod)
         self._scheds = {}
+        self._natives = {}
+
+    def _model_timesteps_host(self, indices):
+        """Model timesteps of table indices (identity; SpacedDiffusion: timestep_map)."""
+        return list(indices)
 
     # -- model wrapping (identity here; SpacedDiffusion remaps) -------------------
     def _map_timesteps(self, t):
@@ -258,21 +298,85 @@ class GaussianDiffusion:
             indices = tqdm(indices)
         B = shape[0]
         ts = torch.arange(self.num_timesteps, dtype=torch.int64, device=device)
+        self._clear_range_flag(model, device)
         for k, i in enumerate(indices):
             t = ts[i:i + 1].expand(B).contiguous()
             nz = None if step_noise is None else step_noise[k]
             with torch.no_grad():
                 out = self._step(kind, model, img, t, clip_denoised, denoised_fn, cond_fn, model_kwargs, nz,
                                  seed, k, eta, offset)
-            if k == len(indices) - 1:
-                check_model_range(model, device)   # once per loop: one stream sync
+            if (k + 1) % RANGE_CHECK_EVERY == 0 or k == len(indices) - 1:
+                check_model_range(model, device)   # every RANGE_CHECK_EVERY steps: one stream sync
             yield out
             img = out["sample"]
+
+    @staticmethod
+    def _clear_range_flag(model, device):
+        """Drop a range-guard flag an earlier call left set, so a loop reports only its own steps."""
+        fn = getattr(model, "clear_range_flag", None)
+        if callable(fn):
+            fn(device)
+
+    def _native_ok(self, model, denoised_fn, cond_fn, model_kwargs, step_noise, progress):
+        from .unet import UNetModel
+        return (NATIVE_MODE > 0 and isinstance(model, UNetModel) and denoised_fn is None and cond_fn is None
+                and not model_kwargs and step_noise is None and not progress and not self.rescale_timesteps)
+
+    def _native_loop(self, kind, model, shape, noise, clip_denoised, device, eta, seed, sample_offset):
+        """The whole reverse loop on the device (csrc/sampler.hip): bit-identical to
+        _loop with Philox noise, without per-step host work."""
+        self._check_mean_type()
+        if device is None:
+            device = next(model.parameters()).device
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise _lib.CfdError("the HIP sampler runs on the GPU only; move the model to a HIP device")
+        lib = _lib.lib()
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        B = shape[0]
+        per_sample = int(np.prod(shape[1:]))
+        offset = sample_offset * per_sample
+        if offset % 4:
+            raise ValueError("sharded sampling needs (elements per sample * first sample) % 4 == 0")
+        if tuple(shape[1:]) != (model.in_channels, model.image_size, model.image_size):
+            raise ValueError(f"shape {tuple(shape)} does not match the model's input")
+        if noise is not None:
+            img = noise.to(device=device, dtype=torch.float32).contiguous()
+        else:
+            img = torch.empty(*shape, dtype=torch.float32, device=device)
+            _lib.check(lib.cfd_randn(_lib.ptr(img), img.numel(), seed, 1 << 40, offset, _lib.stream_of(device)),
+                       "cfd_randn")
+        h = model._handle(device)   # uploads changed parameters, sets the compute mode
+        sched = self._sched(device, eta)
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        key = (id(model), dev, kind, bool(clip_denoised), float(eta), B, NATIVE_MODE, GRAPH_UNROLL)
+        nl = self._natives.get(key)
+        if nl is None or nl.model is not model:
+            tidx = list(range(self.num_timesteps))[::-1]
+            with torch.cuda.device(dev):
+                nl = _NativeLoop(model, sched, h, kind, clip_denoised, B, per_sample, tidx,
+                                 self._model_timesteps_host(tidx), NATIVE_MODE >= 2, GRAPH_UNROLL)
+            # one loop per (model, device): a new batch size / mode replaces the old one and its buffers
+            self._natives = {k: v for k, v in self._natives.items() if k[:2] != key[:2]}
+            self._natives[key] = nl
+        out = torch.empty_like(img)
+        self._clear_range_flag(model, device)
+        n = self.num_timesteps
+        for k0 in range(0, n, RANGE_CHECK_EVERY):
+            k1 = min(n, k0 + RANGE_CHECK_EVERY)
+            nl.run(img if k0 == 0 else None, out if k1 == n else None, k0, k1, seed, offset, device)
+            check_model_range(model, device)
+        return out
 
     def p_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
                       model_kwargs=None, device=None, progress=False, step_noise=None, seed=None, sample_offset=0):
         """gaussian_diffusion.py:441-485.  ``sample_offset``: index of this call's first
-        sample in a larger (sharded) batch, so the Philox noise equals the unsharded run's."""
+        sample in a larger (sharded) batch, so the Philox noise equals the unsharded run's.
+        With Philox noise and a HIP UNetModel the loop runs natively (one HIP graph
+        per step, csrc/sampler.hip); explicit step_noise / progress use the Python loop."""
+        if self._native_ok(model, denoised_fn, cond_fn, model_kwargs, step_noise, progress):
+            return self._native_loop(STEP_DDPM, model, shape, noise, clip_denoised, device, 0.0, seed, sample_offset)
         final = None
         for s in self.p_sample_loop_progressive(model, shape, noise, clip_denoised, denoised_fn, cond_fn,
                                                 model_kwargs, device, progress, step_noise, seed, sample_offset):
@@ -289,7 +393,9 @@ class GaussianDiffusion:
     def ddim_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
                          model_kwargs=None, device=None, progress=False, eta=0.0, step_noise=None, seed=None,
                          sample_offset=0):
-        """gaussian_diffusion.py:625-662."""
+        """gaussian_diffusion.py:625-662 (native loop as p_sample_loop)."""
+        if self._native_ok(model, denoised_fn, cond_fn, model_kwargs, step_noise, progress):
+            return self._native_loop(STEP_DDIM, model, shape, noise, clip_denoised, device, eta, seed, sample_offset)
         final = None
         for s in self.ddim_sample_loop_progressive(model, shape, noise, clip_denoised, denoised_fn, cond_fn,
                                                    model_kwargs, device, progress, eta, step_noise, seed,

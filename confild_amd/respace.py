@@ -51,6 +51,9 @@ class SpacedDiffusion(GaussianDiffusion):
         super().__init__(**kwargs)
         self._maps = {}
 
+    def _model_timesteps_host(self, indices):
+        return [self.timestep_map[i] for i in indices]
+
     def _map_timesteps(self, t):
         dev = t.device
         m = self._maps.get(dev)

@@ -328,6 +328,18 @@ class UNetModel(nn.Module):
         warnings.warn(f"U-Net produced a non-finite eps ({self.compute} compute)", RuntimeWarning, stacklevel=2)
         return False
 
+    def clear_range_flag(self, device=None):
+        """Clears the range-guard flag without acting on it (a loop starting fresh)."""
+        dev = torch.device(device) if device is not None else next(self.parameters()).device
+        if dev.type != "cuda":
+            return
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        entry = self._handles.get(idx)
+        if entry is not None:
+            flag = C.c_int(0)
+            _lib.check(_lib.load().cfd_unet_check_finite(entry[0], C.byref(flag), _lib.stream_of(dev)),
+                       "cfd_unet_check_finite")
+
     # -- input-gradient (DPS adjoint) ---------------------------------------------
     def forward_tape(self, x: torch.Tensor, timesteps: torch.Tensor) -> torch.Tensor:
         """forward() that also records the activations for input_vjp (bit-identical eps)."""

@@ -139,6 +139,29 @@ int  cfd_sched_step(const cfd_sched* s, int kind, int clip, const float* x, cons
                     const int64_t* t, const float* noise, uint64_t seed, uint64_t counter,
                     uint64_t offset, float* x_out, float* xstart_out, int64_t n_per_sample, int B,
                     void* stream);
+/* Native reverse loop (p_sample_loop / ddim_sample_loop, gaussian_diffusion.py:
+ * 441-535 / 625-707, with Philox noise): per step the timestep advance, the U-Net
+ * forward and the K6 epilogue, with no host work between steps.  graph != 0
+ * captures the step once into a HIP graph (`unroll` steps per graph, 1..64) and
+ * replays it; the step's timesteps and Philox counter live in device memory.
+ * host_tidx[k] / host_tmodel[k]: coefficient-table index / model timestep
+ * (timestep_map) of step k in loop order.  The sampler owns its state, eps and
+ * U-Net workspace; `unet` and `sched` must outlive it.  Parameters set on
+ * `unet` later and compute-mode changes are seen (the graph is re-captured
+ * when the handle changed since the last capture).
+ * cfd_sampler_run: steps [k0, k1) of the loop; x_in (B * n_per_sample) is
+ * copied in first unless NULL (continue from the state), x_out receives the
+ * state afterwards unless NULL.  Step k draws Philox(seed, counter = k) at
+ * stream position offset + element (offset % 4 == 0), exactly as
+ * cfd_sched_step with counter k, so the result is bit-identical to a host loop
+ * of cfd_unet_forward + cfd_sched_step. */
+typedef struct cfd_sampler cfd_sampler;
+int  cfd_sampler_create(const cfd_unet* unet, const cfd_sched* sched, int kind, int clip, int B,
+                        int64_t n_per_sample, int n_steps, const int64_t* host_tidx, const int64_t* host_tmodel,
+                        int graph, int unroll, cfd_sampler** out);
+void cfd_sampler_destroy(cfd_sampler* sp);
+int  cfd_sampler_run(cfd_sampler* sp, const float* x_in, float* x_out, int k0, int k1, uint64_t seed,
+                     uint64_t offset, void* stream);
 /* n standard normals from Philox4x32-10 (seed, counter) at stream positions
  * offset .. offset+n-1 (offset % 4 == 0): the device-side stand-in for th.randn
  * (gaussian_diffusion.py:513). */

@@ -1,0 +1,56 @@
+"""Timing probe of the reverse loop per step: Python loop vs native loop vs
+captured HIP graphs (CFD_SAMPLER modes 0/1/2, unroll), at the config-A (32^2,
+mult 1,2,3,4, DDIM-50, B = 1) and config-B (64^2, B = 1 / 8) shapes.
+
+  python tools/loop_probe.py            # prints one JSON line per (config, B, mode)
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from confild_amd import gaussian_diffusion as gd  # noqa: E402
+from confild_amd import synth  # noqa: E402
+from confild_amd.script_util import create_gaussian_diffusion, create_model  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def model(size, mult):
+    m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                     attention_resolutions="32,16,8", channel_mult=mult)
+    sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return m.to(DEV)
+
+
+def main():
+    cases = [("A", 32, "1,2,3,4", "ddim50", True, 1), ("B1", 64, "", "256", False, 1),
+             ("B8", 64, "", "256", False, 8)]
+    only = sys.argv[1:]
+    for name, size, mult, resp, ddim, B in cases:
+        if only and name not in only:
+            continue
+        m = model(size, mult)
+        d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=resp)
+        loop = d.ddim_sample_loop if ddim else d.p_sample_loop
+        for mode, unroll in ((0, 1), (1, 1), (2, 1), (2, 4), (2, 16)):
+            gd.NATIVE_MODE, gd.GRAPH_UNROLL = mode, unroll
+            loop(m, (B, 1, size, size), seed=1)   # warm (capture)
+            torch.cuda.synchronize()
+            reps = 3
+            t0 = time.perf_counter()
+            for r in range(reps):
+                out = loop(m, (B, 1, size, size), seed=2 + r)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / reps
+            print(json.dumps({"case": name, "B": B, "mode": mode, "unroll": unroll, "steps": d.num_timesteps,
+                              "loop_s": dt, "ms_per_step": dt / d.num_timesteps * 1e3,
+                              "finite": bool(torch.isfinite(out).all())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
