@@ -112,6 +112,32 @@ def siren_flops_per_pair(d, L, c, nh, H):
 # ---------------------------------------------------------------------------
 # distributed plumbing
 # ---------------------------------------------------------------------------
+def rank_env(n, rank, port):
+    """Environment of rank `rank` of an n-rank single-node job (what torchrun sets)."""
+    return {"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+            "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+            "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")}
+
+
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` without a launcher: start N rank processes of this
+    script (one per GPU, the torchrun environment) and return the job's exit
+    code.  Runs before anything touches HIP in this process (no exec: the ranks
+    are children); rank 0's JSON line reaches stdout through the inherited pipe."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(rank_env(n, r, port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
 def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -322,7 +348,8 @@ def main_uncond(args, rank, world, dev):
                                  "f16 dense MFMA peak / 3 (split-f16 convolutions)",
                                  "unit": "TFLOP/s", "frac": ua / upeak, "flops": uf, "ms": unet_ms,
                                  "ms_per_forward": unet_ms / nsteps},
-               "cpu_baseline": None}
+               "cpu_baseline": None if args.no_cpu_baseline or world > 1 else cpu_baseline(args.config),
+               "rccl_ranks": world}
         print(json.dumps(rec), flush=True)
     if world > 1:
         import torch.distributed as dist
@@ -369,11 +396,11 @@ def c_inputs(rank, world, n_coords, n_latents, L):
     return coords, lat, ymax, ymin, (s, e)
 
 
-def b_shards(scaling, world):
-    """Config B sample shards [(start, count)] per rank: 8 per GPU (weak) or the
-    global batch of 8 split (strong)."""
+def b_shards(scaling, world, per_gpu=B):
+    """Config B sample shards [(start, count)] per rank: `per_gpu` (default 8) per
+    GPU (weak) or the global batch of 8 split (strong)."""
     from confild_amd import dist as cdist
-    glob = B * world if scaling == "weak" else B
+    glob = per_gpu * world if scaling == "weak" else B
     if glob < world:
         raise ValueError(f"strong scaling needs a global batch >= world size ({glob} < {world})")
     return [(cdist.shard_range(glob, r, world)[0],
@@ -482,59 +509,143 @@ def _time_loop(fn, n_min, budget_s):
     return (time.perf_counter() - t0) / n, n
 
 
+def _unet_oracle(size, mult):
+    from confild_amd import synth
+    from oracle import unet as ou
+    cfg = ou.Config(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                    attention_resolutions="32,16,8", channel_mult=mult)
+    sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(1234, ou.param_shapes(cfg)).items()}
+    return cfg, sd
+
+
+def _siren_oracle(c):
+    from confild_amd import synth
+    return {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"],
+                                                                      c["H"]).items()}
+
+
+def _decode_rate(c, npts, nl):
+    """Seconds per (coordinate, latent) pair of the oracle decode, one chunk."""
+    from oracle import siren as osn
+    ssd = _siren_oracle(c)
+    d = c["d"]
+    coords = torch.rand(npts, d)
+    lat = torch.randn(nl, c["L"])
+    one, mone = torch.ones(1, d), -torch.ones(1, c["c"])
+    with torch.no_grad():
+        osn.decode(ssd, coords[:1024], lat[:1], one, torch.zeros(1, d), torch.ones(1, c["c"]), mone)
+        t0 = time.perf_counter()
+        osn.decode(ssd, coords, lat, one, torch.zeros(1, d), torch.ones(1, c["c"]), mone)
+        dec_s = time.perf_counter() - t0
+    return dec_s / (npts * nl), dec_s, npts * nl
+
+
 def cpu_baseline(config):
     """The oracle (torch CPU restatement of the reference path, the same aten ops
     in the same order) on all physical cores this process may use (SURVEY 8d,
-    BASELINE.md section 3): 8 U-Net sampler steps at B = 8 and one decode chunk
-    of >= 2^20 (coordinate, latent) pairs, measured; fields/s extrapolated
-    linearly (the per-step and per-pair costs are constant)."""
+    BASELINE.md section 3), on a bounded sample of the line's workload:
+      A      the whole DDIM-50 loop + de-normalisation + decode, end to end, best of 3;
+      B / E  8 (B) / 2 (E) U-Net forwards at B = 8 and one decode chunk, extrapolated
+             linearly (the per-step and per-pair costs are constant);
+      C      one decode chunk of 2^20 pairs, extrapolated;
+      D / Case4  k guided steps of one chain (U-Net forward + autograd through the
+             Case4 operator and the U-Net), extrapolated to it/s.
+    The measured parts and the extrapolation are separate fields."""
     from confild_amd import synth
-    from oracle import siren as osn
+    from oracle import diffusion as od
     from oracle import unet as ou
     info, threads = _cpu_info()
     torch.set_num_threads(threads)
     out = {"unit": "fields/s", "cores": threads, "kind": "port", "torch": torch.__version__, **info}
-    if config == "B":
-        cfg = ou.Config(image_size=S, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
-                        attention_resolutions="32,16,8")
-        sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(1234, ou.param_shapes(cfg)).items()}
-        x = torch.randn(B, 1, S, S)
+    if config == "A":
+        c = UNCOND_CFG["A"]
+        cfg, sd = _unet_oracle(c["size"], c["channel_mult"])
+        ssd = _siren_oracle(c["siren"])
+        from oracle import siren as osn
+        tb = od.Tables(1000, "cosine", c["respacing"])
+        Sz, sc = c["size"], c["siren"]
+        coords = torch.from_numpy(synth.uniform(7, "A/coords", (c["coords"], 2), 0.0, 1.0))
+        ymax = torch.from_numpy(synth.uniform(9, "ymax", (1, c["coords"], sc["c"]), 0.5, 2.0))
+        ymin = -torch.from_numpy(synth.uniform(9, "ymin", (1, c["coords"], sc["c"]), 0.5, 2.0))
+
+        def run():
+            g = torch.Generator().manual_seed(42)
+            x0 = torch.randn(1, 1, Sz, Sz, generator=g)
+            noise = [torch.randn(1, 1, Sz, Sz, generator=g) for _ in range(tb.num_timesteps)]
+            with torch.no_grad():
+                lat, _ = od.sample_loop(tb, lambda x, t: ou.forward(sd, cfg, x, t), x0, noise, kind="ddim")
+                den = (lat[:, 0] + 1) * (1.5 - -1.5) / 2 + -1.5
+                return osn.decode(ssd, coords, den.reshape(Sz, Sz), torch.ones(1, 2), torch.zeros(1, 2), ymax, ymin)
+        times = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            f = run()
+            times.append(time.perf_counter() - t0)
+        assert torch.isfinite(f).all()
+        out["measured"] = {"end_to_end_s": times, "best_s": min(times)}
+        out["value"] = 1.0 / min(times)
+        out["sample"] = (f"oracle on {threads} threads: the whole config-A pipeline (DDIM-50 at 32^2 B=1, "
+                         f"de-normalisation, decode of 32 rows x 1000 coords), best of 3, no extrapolation")
+        return out
+    if config in ("D", "Case4"):
+        from confild_amd.normalize import Normalizer_ts  # noqa: F401  (shapes only)
+        from oracle import dps as odps
+        c = DPS_CFG[config]
+        mult = c["channel_mult"].replace(" ", "")
+        cfg, sd = _unet_oracle(c["size"], mult)
+        d, L, co, nh, H = c["siren"]
+        ssd = _siren_oracle(dict(d=d, L=L, c=co, nh=nh, H=H))
+        tb = od.Tables(1000, "cosine", c["respacing"])
+        Sz = c["size"]
+        coords = torch.from_numpy(synth.uniform(5, "dps/sensors", (10, d), 0.0, 1.0))
+        one_d, zero_d = torch.ones(1, d), torch.zeros(1, d)
+        yx, yn = torch.full((co,), 2.0), torch.full((co,), -2.0)
+        vx, vn = torch.full((L,), 1.5), torch.full((L,), -1.5)
+        op = lambda x0: odps.case4_forward(ssd, coords, one_d, zero_d, yx, yn, vx, vn, x0)  # noqa: E731
+        unet = lambda x, t: ou.forward(sd, cfg, x, t)  # noqa: E731
+        x = torch.from_numpy(synth.normal(1000, "dps/xT", (1, 1, Sz, L)))
+        with torch.no_grad():
+            y = op(torch.from_numpy(synth.uniform(6, "dps/xtrue", (1, 1, Sz, L), -0.9, 0.9)))
+        k = 4 if config == "D" else 2
+        odps.dps_step(tb, unet, op, x, tb.num_timesteps - 1, y, torch.randn_like(x), 1.0)   # warm
+        t0 = time.perf_counter()
+        for j in range(k):
+            x = odps.dps_step(tb, unet, op, x, tb.num_timesteps - 1 - j, y, torch.randn_like(x), 1.0)[0]
+        dt = (time.perf_counter() - t0) / k
+        out.update(unit="it/s", value=1.0 / dt, measured={"guided_steps": k, "s_per_step": dt, "chains": 1},
+                   sample=(f"oracle on {threads} threads: {k} guided DPS steps of one chain ({Sz}^2 U-Net forward "
+                           f"+ autograd through the Case4 operator at 10 sensors and the U-Net), it/s = 1 / s per "
+                           f"step (independent chains: the rate per chain)"))
+        return out
+    if config in ("B", "E"):
+        if config == "B":
+            cfg, sd = _unet_oracle(S, "")
+            nf_c, size, nb, steps, rows, npts_field = CNF_B, S, 8, 256, S, GRID ** 3
+        else:
+            e = UNCOND_CFG["E"]
+            cfg, sd = _unet_oracle(e["size"], "")
+            nf_c, size, nb, steps, rows, npts_field = e["siren"], e["size"], 2, 1000, e["size"], e["coords"]
+        x = torch.randn(B, 1, size, size)
         t = torch.full((B,), 500, dtype=torch.int64)
         with torch.no_grad():
-            unet_step, nstep = _time_loop(lambda: ou.forward(sd, cfg, x, t), 8, 0.0)
-        c = CNF_B
-        npts, nl = 65536, 16
-    else:
-        unet_step, nstep = 0.0, 0
-        c = CNF_C
-        npts, nl = 65536, 16
-    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, c["d"], c["L"], c["c"], c["nh"],
-                                                                      c["H"]).items()}
-    coords = torch.rand(npts, 3)
-    lat = torch.randn(nl, c["L"])
-    one, mone = torch.ones(1, 3), -torch.ones(1, 3)
-    with torch.no_grad():
-        osn.decode(ssd, coords[:1024], lat[:1], one, torch.zeros(1, 3), one, mone)
-        t0 = time.perf_counter()
-        osn.decode(ssd, coords, lat, one, torch.zeros(1, 3), one, mone)
-        dec_s = time.perf_counter() - t0
-    pairs = npts * nl
-    pair_s = dec_s / pairs
-    if config == "B":
-        per_field = 256 * unet_step / B + S * GRID ** 3 * pair_s
+            unet_step, nstep = _time_loop(lambda: ou.forward(sd, cfg, x, t), nb, 0.0)
+        pair_s, dec_s, pairs = _decode_rate(nf_c, 65536, 16)
+        per_field = steps * unet_step / B + rows * npts_field * pair_s
         out["measured"] = {"unet_forward_b8_s": unet_step, "unet_forwards": nstep,
                            "decode_pairs": pairs, "decode_s": dec_s, "ns_per_pair": pair_s * 1e9}
-        out["extrapolated"] = {"unet_s_per_field": 256 * unet_step / B, "decode_s_per_field": S * GRID ** 3 * pair_s,
-                               "s_per_field": per_field}
-        out["sample"] = (f"oracle on {threads} threads: {nstep} U-Net forwards at B={B} ({unet_step:.3f} s each) + "
-                         f"one decode of {nl} latents x {npts} coords ({pairs} pairs, {dec_s:.1f} s); extrapolated "
-                         f"to 256 steps per {B} samples + {S} x {GRID ** 3} pairs per field")
-    else:
-        per_field = C_COORDS * pair_s
-        out["measured"] = {"decode_pairs": pairs, "decode_s": dec_s, "ns_per_pair": pair_s * 1e9}
-        out["extrapolated"] = {"s_per_field": per_field}
-        out["sample"] = (f"oracle on {threads} threads: one decode of {nl} latents x {npts} coords ({pairs} pairs, "
-                         f"{dec_s:.1f} s); extrapolated to {C_COORDS} coords per field")
+        out["extrapolated"] = {"unet_s_per_field": steps * unet_step / B,
+                               "decode_s_per_field": rows * npts_field * pair_s, "s_per_field": per_field}
+        out["sample"] = (f"oracle on {threads} threads (fp32; the reference has no bf16 path): {nstep} U-Net forwards "
+                         f"at B={B} ({unet_step:.3f} s each) + one decode of {pairs} pairs ({dec_s:.1f} s); "
+                         f"extrapolated to {steps} steps per {B} samples + {rows} x {npts_field} pairs per field")
+        out["value"] = 1.0 / per_field
+        return out
+    pair_s, dec_s, pairs = _decode_rate(CNF_C, 65536, 16)
+    per_field = C_COORDS * pair_s
+    out["measured"] = {"decode_pairs": pairs, "decode_s": dec_s, "ns_per_pair": pair_s * 1e9}
+    out["extrapolated"] = {"s_per_field": per_field}
+    out["sample"] = (f"oracle on {threads} threads: one decode of {pairs} pairs ({dec_s:.1f} s); extrapolated to "
+                     f"{C_COORDS} coords per field")
     out["value"] = 1.0 / per_field
     return out
 
@@ -555,7 +666,23 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--siren-compute", choices=["split_f16", "f32"], default="split_f16")
     ap.add_argument("--unet-compute", choices=["split_f16", "fp32"], default="split_f16")
+    ap.add_argument("--per-gpu-batch", type=int, default=0,
+                    help="B: samples per GPU in weak scaling (0: config B's 8); 1 = the per-rank share of the "
+                         "8-GPU strong point")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="print each rank's launch environment and exit before any GPU call (tests)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.launch_check:   # the parent has not initialised HIP when it starts the ranks
+            print(json.dumps({"parent_hip_initialized": bool(torch.cuda.is_initialized())}), flush=True)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus and "--gpus" in sys.argv:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    if args.launch_check:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}),
+              flush=True)
+        return
 
     rank, world, dev = init_dist()
     from confild_amd import dist as cdist
@@ -568,7 +695,7 @@ def main():
     if args.config == "B":
         o = setup_B(dev, rank, world, args.siren_compute, args.unet_compute)
         nf = o["nf"]
-        shards = b_shards(args.scaling, world)
+        shards = b_shards(args.scaling, world, args.per_gpu_batch or B)
         glob = sum(cnt for _, cnt in shards)
         start, count = shards[rank]
         sizes = [cnt * S for _, cnt in shards]
@@ -576,6 +703,27 @@ def main():
         def one(k, ev=None):
             f = step_B(o, dev, seed=10 ** 6 + k, start=start, count=count, ev=ev)
             return gather_to_root(f, 0, sizes, world) if gather else f
+
+        def strong_point():
+            """Config B's global batch of 8 split over the ranks (the strong-scaling
+            point), timed like the main line, for the nested "strong" object."""
+            sh = b_shards("strong", world)
+            st_, cn = sh[rank]
+            sz = [c_ * S for _, c_ in sh]
+
+            def f(k):
+                r = step_B(o, dev, seed=2 * 10 ** 6 + k, start=st_, count=cn)
+                return gather_to_root(r, 0, sz, world) if gather else r
+            for w in range(args.warmup):
+                f(-1 - w)
+            barrier(dev, world)
+            t0 = time.perf_counter()
+            for k in range(args.steps):
+                f(k)
+            barrier(dev, world)
+            el = max_over_ranks(time.perf_counter() - t0, dev, world)
+            return {"value": B * args.steps / el, "unit": "fields/s", "ms_per_step": el / args.steps * 1e3,
+                    "global_batch": B, "per_gpu": [c_ for _, c_ in sh], "scaling": "strong"}
         c = CNF_B
         npts = GRID ** 3
         rows_local = count * S
@@ -618,11 +766,12 @@ def main():
     achieved = flops / (dec_ms / 1e3) / 1e12
     if rank == 0 and out is not None:
         assert torch.isfinite(out).all().item(), "non-finite output"
+    strong = strong_point() if args.config == "B" and world > 1 and args.scaling == "weak" else None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.config)
-        par = (f"dp{world} ({'8 samples per GPU' if args.scaling == 'weak' else 'global batch 8 split'}"
+        par = (f"dp{world} ({f'{count} samples per GPU' if args.scaling == 'weak' else 'global batch 8 split'}"
                f"{', fields gathered to rank 0' if gather else ''})") if args.config == "B" else \
             f"coord-sharded over {world} GPU(s){', slabs gathered to rank 0' if gather else ''}"
         if args.config == "B":
@@ -659,7 +808,10 @@ def main():
                                                 "(tools/mfma_chain.cpp, profiles/r02_mfma_chain.json)"}
                             if mode == "split_f16" else {})},
             "cpu_baseline": cpu,
+            "rccl_ranks": world,
         }
+        if strong is not None:
+            rec["strong"] = strong
         if args.config == "B":
             uf = count * UNET_FLOPS_PER_SAMPLE * 256
             ua = uf / (unet_ms / 1e3) / 1e12
@@ -725,7 +877,9 @@ def main_dps(args, rank, world, dev):
                           "parallelism": f"dp{world} (independent chains)"},
                "reference_published": ("9.26-9.35 it/s at one chain, unstated NVIDIA GPU "
                                        "(inference_phy_random_sensor.ipynb:321-330)") if args.config == "Case4" else None,
-               "per_chain_it_s": its / (batch * world)}
+               "per_chain_it_s": its / (batch * world),
+               "cpu_baseline": None if args.no_cpu_baseline or world > 1 else cpu_baseline(args.config),
+               "rccl_ranks": world}
         print(json.dumps(rec), flush=True)
     if world > 1:
         import torch.distributed as dist

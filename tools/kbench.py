@@ -57,10 +57,10 @@ def bench_siren(latents=64, npts=64 ** 3, dims=(3, 64, 3, 15, 384), iters=3, com
                       "tflops": flops / (best / 1e3) / 1e12}), flush=True)
 
 
-def bench_unet(batch=8, size=64, iters=10, bf16=False, compute=None):
+def bench_unet(batch=8, size=64, iters=10, bf16=False, compute=None, mult=""):
     from confild_amd.script_util import create_model
     m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
-                     attention_resolutions="32,16,8", use_bf16=bf16)
+                     attention_resolutions="32,16,8", use_bf16=bf16, channel_mult=mult)
     sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     m.to(DEV)
@@ -124,6 +124,7 @@ if __name__ == "__main__":
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--mult", default="", help="U-Net channel_mult (32^2 needs one: 1,2,3,4)")
     ap.add_argument("--compute", choices=["f32", "split_f16"], default=None)
     ap.add_argument("--unet-compute", choices=["fp32", "split_f16", "bf16"], default=None)
     ap.add_argument("--dims", default="3,64,3,15,384", help="SIREN d,L,c,nh,H")
@@ -131,6 +132,6 @@ if __name__ == "__main__":
     if a.what in ("siren", "sweep"):
         bench_siren(a.latents, dims=tuple(int(v) for v in a.dims.split(",")), compute=a.compute)
     if a.what in ("unet", "sweep"):
-        bench_unet(a.batch, a.size, bf16=a.bf16, compute=a.unet_compute)
+        bench_unet(a.batch, a.size, bf16=a.bf16, compute=a.unet_compute, mult=a.mult)
     if a.what == "dps":
         bench_dps(a.batch, a.size)
