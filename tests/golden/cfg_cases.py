@@ -18,6 +18,13 @@ TRAJ_B = dict(tag="trajB", seed=1234, B=1, image_size=64, respacing="256",
                         num_head_channels=64, attention_resolutions="32,16,8"),
               checkpoints=(0, 1, 2, 4, 8, 16, 32, 64, 128, 192, 240, 250, 254, 255))
 
+# config E (configs[4]): Case3 uncond U-Net 128^2 (default mult 1,1,2,3,4), the full
+# 1000-step DDPM schedule: two 20-step segments of the reference's own p_sample,
+# (start index, steps) -- the loop's first steps and its last
+TRAJ_E = dict(tag="trajE", seed=1234, image_size=128, segments=((999, 20), (19, 20)), keep=(0, 1, 2, 4, 9, 14, 19),
+              unet=dict(image_size=128, num_channels=128, num_res_blocks=2, channel_mult=None, num_heads=4,
+                        num_head_channels=64, attention_resolutions="32,16,8"))
+
 # config A (configs[0]): Case1 uncond 32^2 mult (1,2,3,4), DDIM-50, 1k-coord decode
 CFG_A = dict(tag="cfgA", seed=1234, image_size=32, respacing="ddim50", vmax=1.5, vmin=-1.5,
              unet=dict(image_size=32, num_channels=128, num_res_blocks=2, channel_mult="1,2,3,4", num_heads=4,
@@ -35,6 +42,10 @@ DPS_D = dict(tag="dpsD", seed=1234, respacing="256", scale=1.0, Ns=10, indices=(
 CASE4_OP = dict(seed=77, T=384, L=384, Ns=10, batch_size=384, siren_seed=4242, unet_seed=1234, dps_index=500,
                 unet=dict(image_size=384, num_channels=128, num_res_blocks=2, channel_mult="1, 1, 2, 2, 4, 4",
                           num_heads=4, num_head_channels=64, attention_resolutions="32,16,8"))
+
+
+# the real Case4 loop: 10 consecutive DDPM + 'ps' steps at 384^2 (indices 500 .. 491)
+CASE4_STEPS = dict(start=500, n=10)
 
 
 def noise_for(tag: str, k: int, shape) -> np.ndarray:

@@ -4,7 +4,7 @@ REFERENCE (round 2: parity at config widths, not just fixture scale).
 Run in the build container only (the reference tree does not exist on the GPU
 box):
 
-    python tests/golden/make_golden_cfg.py [trajB] [cfgA] [dpsD] [case4op] [case4dps]
+    python tests/golden/make_golden_cfg.py [trajB] [trajE] [cfgA] [dpsD] [case4op] [case4dps] [case4steps]
 
 Same conventions as make_golden.py / make_golden_dps.py: the reference is
 imported read-only from /root/reference with bytecode writing off, weights are
@@ -18,6 +18,12 @@ Fixtures
   * golden_trajB.npz  -- config B: the full 256-step DDPM reverse loop
     (U/src/gaussian_diffusion.py:441-535, respacing "256") of the 64x64 U-Net
     at B = 1, samples at checkpoint steps + the final latent;
+  * golden_trajE.npz  -- config E: two 20-step segments (indices 999..980 and
+    19..0) of the 1000-step DDPM loop of the 128x128 default-mult U-Net at
+    B = 1 through the reference's p_sample, sample and x0_hat per step;
+  * golden_case4steps.npz -- the real Case4 loop: 10 consecutive DDPM + 'ps'
+    steps (indices 500..491) at 384^2: per step the residual norm, image and
+    x0_hat on a 4x-strided subgrid and whole-image checksums; the final image;
   * golden_cfgA.npz   -- config A end to end: the DDIM-50 loop
     (gaussian_diffusion.py:625-707) of the 32x32 mult-(1,2,3,4) U-Net, the
     latent de-normalisation of scripts/inference.py:59-61 and the CNF decode of
@@ -59,8 +65,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from confild_amd import synth  # noqa: E402
-from cfg_cases import (CASE4_OP, CFG_A, CNF_INF, DPS_D, POST, TRAJ_B, case4_files, cnf_inference_coords,  # noqa: E402
-                       cnf_inference_files, noise_for, post_inputs, unet_weights)
+from cfg_cases import (CASE4_OP, CASE4_STEPS, CFG_A, CNF_INF, DPS_D, POST, TRAJ_B, TRAJ_E, case4_files,  # noqa: E402
+                       cnf_inference_coords, cnf_inference_files, noise_for, post_inputs, unet_weights)
 
 torch.set_num_threads(8)
 
@@ -120,6 +126,34 @@ def gen_trajB():
     _save("golden_trajB.npz", checkpoints=np.array(ks, dtype=np.int64), samples=np.stack([samples[k] for k in ks]),
           pred_xstart=np.stack([x0s[k] for k in ks]), final=final.numpy(),
           timestep_map=np.array(diff.timestep_map, dtype=np.int64))
+
+
+# ---------------------------------------------------------------------------
+def gen_trajE():
+    """config E: two 20-step segments of the 1000-step DDPM loop of the 128^2
+    U-Net (the reference's p_sample, gaussian_diffusion.py:395-439), B = 1."""
+    from src.script_util import create_gaussian_diffusion
+    c = TRAJ_E
+    m = _ref_unet(c["unet"], c["seed"])
+    diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="")
+    S = c["image_size"]
+    shape = (1, 1, S, S)
+    out_arrays = {}
+    t0 = time.time()
+    for start, n in c["segments"]:
+        x = torch.from_numpy(noise_for(f"{c['tag']}/x{start}", 0, shape))
+        samples, x0s = [], []
+        with _Noise(f"{c['tag']}/{start}"), torch.no_grad():
+            for i in range(start, start - n, -1):
+                out = diff.p_sample(m, x, torch.tensor([i]), clip_denoised=True)
+                x = out["sample"]
+                samples.append(x.numpy())
+                x0s.append(out["pred_xstart"].numpy())
+        keep = list(c["keep"])
+        out_arrays[f"samples{start}"] = np.stack([samples[k] for k in keep])
+        out_arrays[f"pred_xstart{start}"] = np.stack([x0s[k] for k in keep])
+    print(f"trajE: {sum(n for _, n in c['segments'])} steps in {time.time() - t0:.1f} s")
+    _save("golden_trajE.npz", keep=np.array(c["keep"], dtype=np.int64), **out_arrays)
 
 
 # ---------------------------------------------------------------------------
@@ -282,6 +316,40 @@ def gen_case4dps():
           nparams=np.int64(sum(int(np.prod(s)) for s in shapes.values())))
 
 
+def gen_case4steps():
+    """The real Case4 loop over CASE4_STEPS["n"] consecutive DDPM + 'ps' steps (the
+    notebook's p_sample_loop body, C/gaussian_diffusion.py:181-199), each with its
+    own recorded noise, from a synth state at index CASE4_STEPS["start"]."""
+    c, cs = CASE4_OP, CASE4_STEPS
+    with tempfile.TemporaryDirectory() as tmp:
+        op = _case4_operator(tmp)
+        kw = c["unet"]
+        from ConditionalDiffusionGeneration.src.guided_diffusion.unet import create_model
+        torch.manual_seed(0)
+        shapes = {k: tuple(v.shape) for k, v in create_model(**kw, model_path="").state_dict().items()}
+        ema = os.path.join(tmp, "ema_0.9999_400000.pt")
+        torch.save({k: torch.from_numpy(v) for k, v in synth.unet_state_dict(c["unet_seed"], shapes).items()}, ema)
+        model = _guided_unet(kw, c["unet_seed"], path=ema)
+        x_true = torch.from_numpy(synth.uniform(c["seed"], "case4op/x", (1, 1, c["T"], c["L"]), -0.95, 0.95))
+        with torch.no_grad():
+            y = op.forward(x_true)
+        sampler = _sampler("")
+        x = torch.from_numpy(synth.normal(c["seed"], f"case4steps/x{cs['start']}", (1, 1, c["T"], c["L"])))
+        imgs, x0s, dists = [], [], []
+        t0 = time.time()
+        for idx in range(cs["start"], cs["start"] - cs["n"], -1):
+            x, x0, _, dist = _ref_dps_step(model, op, sampler, x, idx, y, 1.0, f"case4steps/{idx}")
+            imgs.append(x.numpy())
+            x0s.append(x0.numpy())
+            dists.append(dist)
+            print(f"case4 step {idx}: dist {dist:.5f} ({time.time() - t0:.0f} s)", flush=True)
+    imgs, x0s = np.stack(imgs), np.stack(x0s)
+    # compact: every step on a 4x-strided 96x96 subgrid, whole-image checksums, the final image in full
+    _save("golden_case4steps.npz", dists=np.array(dists), img_sub=imgs[..., ::4, ::4].copy(),
+          x0_sub=x0s[..., ::4, ::4].copy(), img_sum=imgs.astype(np.float64).sum(axis=(1, 2, 3, 4)),
+          img_absmax=np.abs(imgs).max(axis=(1, 2, 3, 4)), img_final=imgs[-1])
+
+
 # ---------------------------------------------------------------------------
 def gen_cnfinf():
     """CNF_inference (inference_function.py:79-304): normal and is_pub checkpoints,
@@ -328,7 +396,7 @@ def gen_post():
     _save("golden_post.npz", frames=frames.astype(np.float32), nan_frame=nanf.astype(np.float32))
 
 
-GEN = {"trajB": gen_trajB, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps,
+GEN = {"trajB": gen_trajB, "trajE": gen_trajE, "case4steps": gen_case4steps, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps,
        "cnfinf": gen_cnfinf, "post": gen_post}
 
 if __name__ == "__main__":

@@ -5,9 +5,10 @@ Two references, on the reference-pinned fixtures:
     conv_gemm fed bf16-rounded (RNE) operands and accumulating in fp32 -- the
     same arithmetic up to summation order, so a tight bound;
   * the fp32 oracle itself: the precision cost of bf16 operands, stated.
-Tolerances (max|diff| / max|ref|): <= 1.5e-2 against the emulation and
-<= 3e-2 against fp32 (measured r01: 4.6e-3 / 6.3e-3 at tiny16, 6.9e-3 / 1.2e-2 at
-small32, 5.5e-3 / 6.4e-3 at the config-E width).  The emulation cannot be
+Tolerances (max|diff| / max|ref|) per topology, about 1.5x the largest value
+measured over rounds 1-2 (emulation / fp32): tiny16 <= 8e-3 / 1e-2 (measured
+4.8e-3 / 6.5e-3), small32 <= 1.5e-2 / 1.7e-2 (1.0e-2 / 1.13e-2), the config-E
+width cfgE128 <= 8e-3 / 1e-2 (5.5e-3 / 6.9e-3).  The emulation cannot be
 matched more tightly: bf16 rounding of fp32 values that differ by an ulp
 (torch's vs this GroupNorm, say) flips roundings near the boundaries, and the
 network amplifies that -- jittering the emulation's pre-rounding values by
@@ -54,6 +55,9 @@ class _Bf16Convs:
         ou.F.conv2d, ou.F.conv1d = self.c2, self.c1
 
 
+BOUNDS = {"tiny16": (8e-3, 1e-2), "small32": (1.5e-2, 1.7e-2), "cfgE128": (8e-3, 1e-2)}
+
+
 @pytest.mark.parametrize("name", ["tiny16", "small32", "cfgE128"])
 def test_bf16_unet_matches_emulation_and_fp32(hip, name):
     g = golden(f"unet_{name}.npz")
@@ -72,8 +76,9 @@ def test_bf16_unet_matches_emulation_and_fp32(hip, name):
     e_emu = float((eps - emu).abs().max() / emu.abs().max())
     e_32 = float((eps - ref32).abs().max() / ref32.abs().max())
     print(f"{name}: bf16 vs emulation {e_emu:.2e}, vs fp32 reference {e_32:.2e}")
-    assert e_emu < 1.5e-2, e_emu
-    assert e_32 < 3e-2, e_32
+    b_emu, b_32 = BOUNDS[name]
+    assert e_emu < b_emu, e_emu
+    assert e_32 < b_32, e_32
     # fp32 mode on the same module is the fp32 path again
     m.set_compute("fp32")
     e_back = float((m(x.to(DEV), t.to(DEV)).cpu() - ref32).abs().max() / ref32.abs().max())
