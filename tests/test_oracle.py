@@ -260,3 +260,58 @@ def test_oracle_case4_operator_from_files(tmp_path):
                                torch.from_numpy(np.load(p["max"])), torch.from_numpy(np.load(p["min"])), x,
                                batch=c["batch_size"])
     assert np.abs(A.numpy() - g["A"]).max() < 2e-5 * max(1.0, float(np.abs(g["A"]).max()))
+
+
+def test_oracle_configE_segment_prefix():
+    """First 4 steps of each config-E segment (128^2 U-Net, 1000-step DDPM)."""
+    cc = _cfg_cases()
+    c = cc.TRAJ_E
+    g = golden("golden_trajE.npz")
+    cfg = ou.Config(**c["unet"])
+    sd = {k: torch.from_numpy(v) for k, v in cc.unet_weights(ou.param_shapes(cfg), c["seed"]).items()}
+    tb = od.Tables(1000, "cosine", "")
+    S = c["image_size"]
+    shape = (1, 1, S, S)
+    keep = [int(k) for k in g["keep"]]
+    with torch.no_grad():
+        for start, _ in c["segments"]:
+            x = torch.from_numpy(cc.noise_for(f"{c['tag']}/x{start}", 0, shape))
+            for k, i in enumerate(range(start, start - 4, -1)):
+                t = torch.full((1,), i, dtype=torch.int64)
+                eps = ou.forward(sd, cfg, x, t)
+                x, x0 = od.ddpm_step(tb, x, t, eps, torch.from_numpy(cc.noise_for(f"{c['tag']}/{start}", k, shape)))
+                if k in keep:
+                    j = keep.index(k)
+                    assert np.abs(x.numpy() - g[f"samples{start}"][j]).max() < 2e-5, (start, k)
+                    amp = max(1.0, float(tb.sqrt_recipm1_alphas_cumprod[i]))
+                    assert np.abs(x0.numpy() - g[f"pred_xstart{start}"][j]).max() < 2e-5 * amp, (start, k)
+
+
+def test_oracle_case4_chain_first_step(tmp_path):
+    """The first step of the real-Case4 10-step chain fixture (384^2 U-Net, the
+    file-built operator) through the oracle's autograd DPS step."""
+    cc = _cfg_cases()
+    c, cs = cc.CASE4_OP, cc.CASE4_STEPS
+    g = golden("golden_case4steps.npz")
+    p = cc.case4_files(str(tmp_path))
+    prm = torch.load(p["normalizer"], weights_only=True)
+    ssd = torch.load(p["ckpt"], weights_only=True)["model_state_dict"]
+    xh, xl = prm["x_normalizer_params"]
+    yh, yl = prm["y_normalizer0u_params"][0][:3], prm["y_normalizer0l_params"][1][:3]
+    coords = torch.from_numpy(np.load(p["coords"])).float()
+    vmax, vmin = torch.from_numpy(np.load(p["max"])), torch.from_numpy(np.load(p["min"]))
+    operator = lambda x0: odps.case4_forward(ssd, coords, xh, xl, yh, yl, vmax, vmin, x0,  # noqa: E731
+                                             batch=c["batch_size"])
+    cfg = ou.Config(**{**c["unet"], "channel_mult": c["unet"]["channel_mult"].replace(" ", "")})
+    sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(c["unet_seed"], ou.param_shapes(cfg)).items()}
+    unet = lambda x, t: ou.forward(sd, cfg, x, t)  # noqa: E731
+    shape = (1, 1, c["T"], c["L"])
+    y = torch.from_numpy(golden("golden_case4op.npz")["A"])
+    x = torch.from_numpy(synth.normal(c["seed"], f"case4steps/x{cs['start']}", shape))
+    idx = cs["start"]
+    nz = torch.from_numpy(cc.noise_for(f"case4steps/{idx}", 0, shape))
+    img, x0, _, norm = odps.dps_step(od.Tables(1000, "cosine", ""), unet, operator, x, idx, y, nz, 1.0)
+    sc = max(1.0, float(np.abs(g["img_sub"][0]).max()))
+    assert np.abs(img[..., ::4, ::4].numpy() - g["img_sub"][0]).max() < 2e-5 * sc
+    assert np.abs(x0[..., ::4, ::4].numpy() - g["x0_sub"][0]).max() < 2e-5
+    assert abs(float(norm) - float(g["dists"][0])) < 1e-5 * float(g["dists"][0])
