@@ -213,6 +213,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    // split-K (gridDim.z > 1): slice z of K, partial sums to C + z * M * ldc
+    const int kspan = K / (int)gridDim.z, kbeg = (int)blockIdx.z * kspan;
+    A += kbeg;
+    Bm += BT ? kbeg : (int64_t)kbeg * ldb;
+    K = kspan;
+    C += (int64_t)blockIdx.z * M * ldc;
     f4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -269,16 +275,45 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
         }
 }
 
+// C[m, n] = sum_z part[z][m, n] (+ bias[n]), z in order
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __restrict__ part, const float* bias,
+                                                                float* __restrict__ C, int M, int N, int ldc,
+                                                                int splits) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)M * N) return;
+    const int64_t m = i / N, n = i - m * N;
+    float s = part[m * ldc + n];
+    for (int z = 1; z < splits; ++z) s += part[((int64_t)z * M + m) * ldc + n];
+    C[m * ldc + n] = bias ? s + bias[n] : s;
+}
+
+// split-K count of a latent-side GEMM: a function of K only (never of M, the
+// latent rows), so a row's result does not depend on how many rows share the call
+static int gemm_splits(int K) {
+    int s = 1;
+    while (s < 16 && K / (2 * s) >= 256 && K % (32 * s) == 0) s *= 2;
+    return s;
+}
+
+// part: scratch of gemm_splits(K) * M * ldc floats (used when that is > 1)
 static void launch_gemm_f32(bool bt, const float* A, int lda, const float* B, int ldb, const float* bias, float* C,
-                            int ldc, int M, int N, int K, hipStream_t st) {
+                            int ldc, int M, int N, int K, hipStream_t st, float* part = nullptr) {
     CFD_REQUIRE(K % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0 && (bt || N % 4 == 0), CFD_ESHAPE,
                 "gemm_f32: K % 16, leading dims % 4");
-    const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(M, 64));
+    const int splits = part ? gemm_splits(K) : 1;
+    const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(M, 64), (unsigned)splits);
+    float* out = splits > 1 ? part : C;
+    const float* b = splits > 1 ? nullptr : bias;
     if (bt)
-        hipLaunchKernelGGL(gemm_f32_kernel<true>, grid, dim3(256), 0, st, A, lda, B, ldb, bias, C, ldc, M, N, K);
+        hipLaunchKernelGGL(gemm_f32_kernel<true>, grid, dim3(256), 0, st, A, lda, B, ldb, b, out, ldc, M, N, K);
     else
-        hipLaunchKernelGGL(gemm_f32_kernel<false>, grid, dim3(256), 0, st, A, lda, B, ldb, bias, C, ldc, M, N, K);
+        hipLaunchKernelGGL(gemm_f32_kernel<false>, grid, dim3(256), 0, st, A, lda, B, ldb, b, out, ldc, M, N, K);
     check_launch("gemm_f32_kernel");
+    if (splits > 1) {
+        hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div((int64_t)M * N, 256)), dim3(256), 0, st,
+                           part, bias, C, M, N, ldc, splits);
+        check_launch("gemm_splitk_reduce_kernel");
+    }
 }
 
 // D (R, nf) = sum over the Ns sensors of delta (R, Ns, nf), in sensor order
@@ -1285,8 +1320,11 @@ extern "C" int cfd_siren_vjp_workspace_bytes(const cfd_siren* h, int64_t Ns, int
     return cfd::guard([&] {
         CFD_REQUIRE(h && bytes && Ns >= 0 && R >= 0, CFD_EARG, "bad argument");
         const size_t nl = h->cfg.num_hidden_layers + 1, H = h->cfg.hidden_features;
-        // FiLM vectors, the tape (pre-activations and deltas), the sensor-summed deltas
-        *bytes = sizeof(float) * (2 * (size_t)R * nl * H + 2 * (size_t)R * Ns * nl * H);
+        // FiLM vectors, the tape (pre-activations and deltas), the sensor-summed deltas,
+        // the latent-gradient GEMM's split-K partials
+        const size_t L = h->cfg.in_latent_features;
+        *bytes = sizeof(float) * (2 * (size_t)R * nl * H + 2 * (size_t)R * Ns * nl * H +
+                                  (size_t)cfd::gemm_splits((int)(nl * H)) * R * L);
     });
 }
 
@@ -1343,7 +1381,7 @@ extern "C" int cfd_siren_tape_vjp(cfd_siren* h, const float* g_out, int64_t Ns, 
             hipLaunchKernelGGL(cfd::sensor_sum_kernel, dim3((unsigned)cfd::ceil_div(R * nf, 256)), dim3(256), 0, st,
                                a.delta, D, (int)Ns, nf, (int64_t)R);
             cfd::check_launch("sensor_sum_kernel");
-            cfd::launch_gemm_f32(false, D, (int)nf, h->V, L, nullptr, g_latents, L, R, L, (int)nf, st);
+            cfd::launch_gemm_f32(false, D, (int)nf, h->V, L, nullptr, g_latents, L, R, L, (int)nf, st, D + R * nf);
         } else {
             const size_t lds = sizeof(float) * (size_t)(nh + 1) * H;
             CFD_REQUIRE(lds <= 160 * 1024, CFD_EARG, "SIREN too deep for the latent-gradient reduction");

@@ -608,7 +608,11 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 rec.lse = aa.lse;
                 flush();
                 if (launch) {
-                    if (h->compute == CFD_COMPUTE_SPLIT_F16 && (at.ch == 32 || at.ch == 64 || at.ch == 128))
+                    // split-f16 attention (fp32-accurate, K4d) in the split and the bf16 modes: the
+                    // reference's fp16 contract runs q.k and a.v in the low precision with an fp32
+                    // softmax (unet.py:349-353), so fp32-level attention is within it; the exact
+                    // fp32-MFMA kernel K4 stays for CFD_COMPUTE_F32
+                    if (h->compute != CFD_COMPUTE_F32 && (at.ch == 32 || at.ch == 64 || at.ch == 128))
                         cfd::launch_attention_split(aa, at.ch, at.heads, B, kvws, st);
                     else
                         cfd::launch_attention(aa, at.ch, at.heads, B, st);

@@ -931,7 +931,8 @@ __global__ __launch_bounds__(256) void conv_out_vec_kernel(ConvArgs a, int LP) {
     const int b = (int)(mm / HW), rem = (int)(mm - (int64_t)b * HW), oy = rem / a.Wout, ox = rem - oy * a.Wout;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     for (int tap = 0; tap < 9; ++tap) {
-        const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+        // tmode: taps mirrored (the input-gradient of the first convolution)
+        const int iy = a.tmode ? oy + 1 - tap / 3 : oy + tap / 3 - 1, ix = a.tmode ? ox + 1 - tap % 3 : ox + tap % 3 - 1;
         if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
         const f4 v = *(const f4*)(a.src1 + (((int64_t)b * a.Hin + iy) * a.Win + ix) * a.C1 + c);
 #pragma unroll
@@ -976,7 +977,8 @@ __global__ __launch_bounds__(256) void conv_in_vec_kernel(ConvArgs a) {
     const int b = (int)(m / HW), rem = (int)(m - (int64_t)b * HW), oy = rem / a.Wout, ox = rem - oy * a.Wout;
     f4 s = {0.f, 0.f, 0.f, 0.f};
     for (int tap = 0; tap < 9; ++tap) {
-        const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+        // tmode: taps mirrored (the input-gradient of the last convolution)
+        const int iy = a.tmode ? oy + 1 - tap / 3 : oy + tap / 3 - 1, ix = a.tmode ? ox + 1 - tap % 3 : ox + tap % 3 - 1;
         if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) continue;
         const float* px = a.src1 + (((int64_t)b * a.Hin + iy) * a.Win + ix) * C1;
         for (int cc = 0; cc < C1; ++cc) {
@@ -1935,7 +1937,7 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
 }
 
 void launch_conv_in(const ConvArgs& a, hipStream_t st) {
-    if (!a.tmode && a.Cout % 4 == 0 && a.C1 <= 4 && (size_t)9 * a.C1 * a.Cout * 4 <= 64 * 1024) {
+    if (a.Cout % 4 == 0 && a.C1 <= 4 && (size_t)9 * a.C1 * a.Cout * 4 <= 64 * 1024) {
         const int64_t n = (int64_t)a.M * (a.Cout / 4);
         hipLaunchKernelGGL(conv_in_vec_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256),
                            sizeof(float) * 9 * a.C1 * a.Cout, st, a);
@@ -1950,7 +1952,7 @@ void launch_conv_in(const ConvArgs& a, hipStream_t st) {
 void launch_conv_out(const ConvArgs& a, hipStream_t st) {
     CFD_REQUIRE(a.Cout <= 4, CFD_ESHAPE, "out_channels must be <= 4");
     const int LP = a.Ctot / 4;
-    if (!a.tmode && a.Ctot % 4 == 0 && a.C1 == a.Ctot && LP >= 1 && LP <= 64 && (LP & (LP - 1)) == 0 &&
+    if (a.Ctot % 4 == 0 && a.C1 == a.Ctot && LP >= 1 && LP <= 64 && (LP & (LP - 1)) == 0 &&
         (size_t)a.Cout * a.K * 4 <= 64 * 1024) {
         const int64_t waves = ceil_div(a.M, 64 / LP);
         hipLaunchKernelGGL(conv_out_vec_kernel, dim3((unsigned)ceil_div(waves, 4)), dim3(256),

@@ -75,8 +75,9 @@ int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
  * remapped through timestep_map, respace.py:123-128), eps (B,1,H,W). */
 /* Convolution operand precision (config E, BASELINE.json configs[4]):
  * CFD_COMPUTE_BF16 rounds both convolution operands to bf16 (RNE) and
- * accumulates in fp32 on v_mfma_f32_16x16x32_bf16; GroupNorm, softmax,
- * attention, the timestep MLP and the 1-channel in/out convolutions stay fp32.
+ * accumulates in fp32 on v_mfma_f32_16x16x32_bf16; GroupNorm, softmax, the
+ * timestep MLP and the 1-channel in/out convolutions stay fp32, attention runs
+ * the fp32-accurate split-f16 kernel.
  * Default CFD_COMPUTE_SPLIT_F16 (fp32-accurate, below); CFD_COMPUTE_F32 is the
  * exact fp32 MFMA path.  This
  * replaces UNetModel's use_fp16 torso conversion (U/src/unet.py:619-633) with
