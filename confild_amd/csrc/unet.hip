@@ -693,6 +693,15 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     // input-gradient of a convolution: dY (Hin x Win, Cin_bwd channels) -> dX (Hout x Wout, cout)
     auto dconv = [&](const float* dy, int cin, int Hin, int Win, const std::string& key, int cout, int Hout, int Wout,
                      int ks, int stride, int pad, int tmode, float* out) {
+        {   // a pack kind runs only in its addressing mode: mirrored taps (3) as a plain
+            // convolution, the transposed pack (1) through TMODE, upsample (2) plain
+            auto it = h->index.find(key);
+            CFD_REQUIRE(it != h->index.end(), CFD_EKEY, "internal: missing conv " + key);
+            const int tp = h->params[it->second].tpack;
+            CFD_REQUIRE((tp == 3 && tmode == 0) || (tp == 1 && tmode == 1) || (tp == 2 && tmode == 0) ||
+                            (tp == 1 && ks == 1),
+                        CFD_ESTATE, "internal: input-gradient pack kind / addressing mismatch at " + key);
+        }
         cfd::ConvArgs a{};
         a.src1 = dy;
         a.C1 = cin;

@@ -1768,8 +1768,10 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // (0 = auto), CFD_CONV_TARGET_WG.
     static const int force_bm = env_int("CFD_CONV_BM", 0);
     static const int target = env_int("CFD_CONV_TARGET_WG", 768);
+    // development: CFD_PLAN_B plans for that batch instead of 8 (small-batch experiments)
+    static const int plan_b = env_int("CFD_PLAN_B", 8);
     ConvPlan p;
-    const int64_t mn = (int64_t)8 * a.Hout * a.Wout;
+    const int64_t mn = (int64_t)plan_b * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;
     auto tiles = [&](int bm) { return ceil_div(mn, bm) * ceil_div(a.Cout, p.bn); };
     p.bm = force_bm ? force_bm : 64;  // 64x128 measured ahead of 128x128 (r01 sweep: 8.76 vs 9.26 ms)
@@ -1884,9 +1886,12 @@ void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st) {
 
 int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defer) {
     ConvPlan p = p0;
-    if (p.kx >= 0) {   // K1x needs 32-bit operand offsets at the real batch; else K1s tiles, same splits
+    // K1x / K1h need 32-bit operand offsets at the real batch; else K1s 128x128 tiles of 8
+    // waves with the same splits (CFD_CONV_FORCE_K1S=1 forces that fallback: tests)
+    static const int force_k1s = env_int("CFD_CONV_FORCE_K1S", 0);
+    if (p.kx >= 0) {
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
-        if (!(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31))) {
+        if (force_k1s || !(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31))) {
             p.kx = -1;
             p.bm = p.bn = 128;
             p.nw = 8;
