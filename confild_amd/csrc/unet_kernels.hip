@@ -1760,6 +1760,14 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
 }
 
 
+// K1h splits chunk ranges of ceil(nch / splits) chunks: drop the splits that
+// would be left with none (they cost a zero partial slab written and read)
+static int even_splits(int nch, int splits) {
+    if (splits <= 1) return 1;
+    const int per = (nch + splits - 1) / splits;
+    return (nch + per - 1) / per;
+}
+
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // Every choice is made from the per-sample shape (as if the batch were 8),
     // never from the actual batch: the split-K count fixes each output's
@@ -1822,6 +1830,7 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
         q.splits = 1;
         while (t * q.splits < 256 && q.splits * 2 <= nch && q.splits < 16) q.splits *= 2;
         while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
+        q.splits = even_splits(nch, q.splits);
         return q;
     }
     if (kx && a.wbf && a.wlo && !a.tmode && kx_shape && a.Cout >= 128 &&
@@ -1843,6 +1852,7 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
             q.splits = 1;
             while (t * q.splits < 256 && q.splits * 2 <= nch && q.splits < 16) q.splits *= 2;
             while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
+            q.splits = even_splits(nch, q.splits);
             return q;
         }
         q.kx = mn >= 2048 ? 2 : 1;

@@ -19,29 +19,46 @@ from confild_amd.script_util import create_gaussian_diffusion, create_model  # n
 DEV = torch.device("cuda", 0)
 
 
-def model(size, mult):
+def model(size, mult, compute="split_f16"):
     m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
                      attention_resolutions="32,16,8", channel_mult=mult)
     sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    return m.to(DEV)
+    return m.to(DEV).set_compute(compute)
+
+
+def forward_ms(m, B, size, iters=20):
+    x = torch.randn(B, 1, size, size, device=DEV)
+    t = torch.full((B,), 500, dtype=torch.int64, device=DEV)
+    m(x, t)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        m(x, t)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e3
 
 
 def main():
-    cases = [("A", 32, "1,2,3,4", "ddim50", True, 1), ("B1", 64, "", "256", False, 1),
-             ("B8", 64, "", "256", False, 8)]
+    cases = [("A", 32, "1,2,3,4", "ddim50", True, 1, "split_f16"), ("B1", 64, "", "256", False, 1, "split_f16"),
+             ("B8", 64, "", "256", False, 8, "split_f16"), ("E100", 128, "", "100", False, 8, "bf16"),
+             ("E1000", 128, "", "", False, 8, "bf16")]
     only = sys.argv[1:]
-    for name, size, mult, resp, ddim, B in cases:
+    modes = ((0, 1), (1, 1), (2, 1), (2, 4), (2, 16))
+    if os.environ.get("LOOP_MODES"):
+        modes = tuple(tuple(int(v) for v in x.split(":")) for x in os.environ["LOOP_MODES"].split(","))
+    for name, size, mult, resp, ddim, B, compute in cases:
         if only and name not in only:
             continue
-        m = model(size, mult)
+        m = model(size, mult, compute)
+        print(json.dumps({"case": name, "forward_ms": forward_ms(m, B, size)}), flush=True)
         d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=resp)
         loop = d.ddim_sample_loop if ddim else d.p_sample_loop
-        for mode, unroll in ((0, 1), (1, 1), (2, 1), (2, 4), (2, 16)):
+        for mode, unroll in modes:
             gd.NATIVE_MODE, gd.GRAPH_UNROLL = mode, unroll
             loop(m, (B, 1, size, size), seed=1)   # warm (capture)
             torch.cuda.synchronize()
-            reps = 3
+            reps = 1 if d.num_timesteps >= 1000 else 3
             t0 = time.perf_counter()
             for r in range(reps):
                 out = loop(m, (B, 1, size, size), seed=2 + r)
