@@ -357,9 +357,10 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // with no partial slab in HBM (split-K over workgroups, gridDim.z, still
 // composes with it).  K order is (chunk, tap) per group -- every output's
 // summation order is a function of the per-sample shape only, as K1x's.  The
-// planner ships BM = 256, KG = 1: 128-pixel blocks in 2 groups (variant 21)
-// measured 0.83-1.07x of it on the config-B shapes, their weight slices serving
-// half the pixels, so the split-K slab they avoid does not pay for itself.
+// planner ships BM = 256, KG = 1: 128-pixel blocks in 2 groups measured
+// 0.83-1.07x of it on the config-B shapes, their weight slices serving half the
+// pixels, so the split-K slab they avoid does not pay for itself (that variant
+// and K1y, an LDS-DMA ring, 0.75-0.84x, were removed in round 3).
 //
 // Measured and not kept (tools/convbench): fragment reads software-
 // pipelined across steps (3-stage ring, 2 halo stages): no change; the timing
@@ -680,259 +681,6 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
         }
 }
 
-// ---------------------------------------------------------------------------
-// K1y: the same GEMM with every operand staged by LDS-DMA into an S-stage LDS
-// ring (buffer_load ... lds: no VGPR staging, S-1 K tiles in flight per
-// workgroup).  The activation tile lands as fp32 (im2col rows gathered per
-// lane, padding taps read as zeros by the buffer range check) and is split into
-// hi/lo f16 as each wave reads its fragments; weights land pre-split.
-// Workgroup 128x128 of 4 waves (one per SIMD), 64x64 wave tiles of 32x32x16
-// MFMAs.  LDS layouts (DMA lane order chosen so the fragment reads are
-// conflict-free): A rows 128 B, 16-B chunk c of row r in slot c ^ ((r>>1)&7);
-// B rows 64 B (xswz).
-__device__ __forceinline__ int yswzA(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
-
-// s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
-constexpr int ywait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
-
-__device__ __forceinline__ void split8_mix(const f4& x0, const f4& x1, h8v& hi, h8v& lo) {
-    unsigned hw[4], lw[4];
-    const float xs[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const float a = xs[2 * w], b = xs[2 * w + 1];
-        hw[w] = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, h2));
-        unsigned l;
-        asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(l) : "v"(a), "v"(hw[w]));
-        asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(hw[w]));
-        lw[w] = l;
-    }
-    hi = __builtin_bit_cast(h8v, (u4){hw[0], hw[1], hw[2], hw[3]});
-    lo = __builtin_bit_cast(h8v, (u4){lw[0], lw[1], lw[2], lw[3]});
-}
-
-// EXP (timing experiments only, wrong results): bit 0 no hi/lo split (A bits
-// reinterpreted), bit 1 no per-tap address arithmetic, bit 2 no A DMA at all
-// KORD: K tile order -- 0 (tap, channel chunk) as the weight packing, 1 (channel
-// chunk, tap): the 9 taps of one 32-channel chunk run back to back, so the
-// activation rows they re-read are still in L1/L2 (the summation order changes,
-// still a function of the per-sample shape only).
-template <int S, int EXP = 0, int KORD = 0>
-__global__ __launch_bounds__(256, 1) void conv_y_kernel(ConvArgs a) {
-    constexpr int BM = 128, BN = 128;
-    constexpr int ABYTES = BM * 32 * 4, BPLANE = BN * 32 * 2, STAGE = ABYTES + 2 * BPLANE;
-    constexpr int PPW = 8;   // DMA pieces per wave per K tile: 4 A + 2 B hi + 2 B lo
-    __shared__ __attribute__((aligned(1024))) char lds[S * STAGE];
-    __shared__ int pixtab[9 * BM];   // source pixel of (tap, tile row), -1: padding
-    typedef __attribute__((address_space(3))) void lds_t;
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    int bx, by, bz;
-    xcd_tile(a.xcd, bx, by, bz);
-    const int m0 = bx * BM, n0 = by * BN;
-    const int HWo = a.Hout * a.Wout;
-
-    // (tap, row) -> source pixel table, once per workgroup
-    const int ntap = a.ks * a.ks;
-    for (int e = threadIdx.x; e < ntap * BM; e += 256) {
-        const int tap = e / BM, r = e - tap * BM;
-        const int dy = tap / a.ks, dx = tap - dy * a.ks;
-        const int m = m0 + r;
-        int pix = -1;
-        if (m < a.M) {
-            const int b = m / HWo, rem = m - b * HWo;
-            const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
-            int iy = (a.up ? oy - a.pad : oy * a.stride - a.pad) + dy;
-            int ix = (a.up ? ox - a.pad : ox * a.stride - a.pad) + dx;
-            bool ok;
-            if (a.up) {
-                ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
-                iy >>= 1;
-                ix >>= 1;
-            } else {
-                ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-            }
-            if (ok) pix = (b * a.Hin + iy) * a.Win + ix;
-        }
-        pixtab[e] = pix;
-    }
-    // A rows of this lane's 4 pieces (piece 4*wave + i covers rows 8 piece .. +7)
-    int a_r[4], a_c16[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        a_r[i] = (4 * wave + i) * 8 + (lane >> 3);
-        a_c16[i] = 16 * ((lane & 7) ^ ((a_r[i] >> 1) & 7));
-    }
-    // B rows of this lane's 2 pieces per plane (piece 2*wave + j covers rows 16 piece .. +15)
-    unsigned b_off[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int r = (2 * wave + j) * 16 + (lane >> 2);
-        const int c = (lane & 3) ^ ((r >> 2) & 3);
-        const int n = n0 + r;
-        b_off[j] = n < a.Cout ? (unsigned)(((int64_t)n * a.K + 8 * c) * 2) : 0x80000000u;
-    }
-    const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR: a VGPR descriptor field costs a readfirstlane loop per load   // input pixels of the whole batch
-    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs2 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
-
-    const int nkt = a.K / 32;
-    const int per = (nkt + gridDim.z - 1) / gridDim.z;
-    const int kt0 = bz * per;
-    const int kt1 = min(nkt, kt0 + per);
-
-    // K position of the next tile to issue: tap, channel base (advanced per issue)
-    int itap, icb;
-    if (KORD == 0) {
-        itap = (kt0 * 32) / a.Ctot;
-        icb = kt0 * 32 - itap * a.Ctot;
-    } else {
-        icb = 32 * (kt0 / ntap);
-        itap = kt0 - (icb / 32) * ntap;
-    }
-    auto issue = [&](int t, int stage) {
-        const int tap = itap, cb = icb;
-        if (KORD == 0) {
-            icb += 32;
-            if (icb == a.Ctot) {
-                icb = 0;
-                ++itap;
-            }
-        } else if (++itap == ntap) {
-            itap = 0;
-            icb += 32;
-        }
-        const bool second = cb >= a.C1;
-        const unsigned csrc4 = 4u * (second ? a.C2 : a.C1), cofs4 = 4u * (second ? cb - a.C1 : cb);
-        const int kb = t * 32;
-        char* sb = lds + stage * STAGE;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if constexpr ((EXP & 4) != 0) continue;
-            if constexpr ((EXP & 2) != 0) {
-                lds_t* dst = (lds_t*)(sb + (4 * wave + i) * 1024);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, dst, 16, a_c16[i] + lane * 64, kb * 4, 0, 0);
-                continue;
-            }
-            const int pix = pixtab[tap * BM + a_r[i]];
-            const unsigned off = pix >= 0 ? __umul24((unsigned)pix, csrc4) + (cofs4 + a_c16[i])
-                                          : 0x80000000u;
-            lds_t* dst = (lds_t*)(sb + (4 * wave + i) * 1024);
-            if (second)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs2, dst, 16, off, 0, 0, 0);
-            else
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, dst, 16, off, 0, 0, 0);
-        }
-        const int kofs = (tap * a.Ctot + cb) * 2;   // bytes of this K tile in a (tap, channel) weight row
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const unsigned off = b_off[j] == 0x80000000u ? b_off[j] : b_off[j] + kofs;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rwh, (lds_t*)(sb + ABYTES + (2 * wave + j) * 1024), 16, off, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rwl, (lds_t*)(sb + ABYTES + BPLANE + (2 * wave + j) * 1024), 16,
-                                                     off, 0, 0, 0);
-        }
-    };
-
-    f16v acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    const int l32 = lane & 31, hsel = lane >> 5;
-    const int arow = wm * 64 + l32, brow = wn * 64 + l32;
-
-    __syncthreads();   // pixtab
-    for (int t = 0; t < S - 1; ++t)
-        if (kt0 + t < kt1) issue(kt0 + t, t);
-    for (int kt = kt0; kt < kt1; ++kt) {
-        const int ahead = min(S - 2, kt1 - 1 - kt);   // tiles issued after kt
-        if (ahead >= 2) __builtin_amdgcn_s_waitcnt(ywait(2 * PPW));
-        else if (ahead == 1) __builtin_amdgcn_s_waitcnt(ywait(PPW));
-        else __builtin_amdgcn_s_waitcnt(ywait(0));
-        __syncthreads();
-        if (kt + S - 1 < kt1) issue(kt + S - 1, (kt - kt0 + S - 1) % S);
-        const char* sb = lds + ((kt - kt0) % S) * STAGE;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            h8v fah[2], fal[2], fbh[2], fbl[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int row = arow + 32 * i;
-                if constexpr ((EXP & 1) != 0) {
-                    fah[i] = *(const h8v*)(sb + yswzA(row, 4 * s + 2 * hsel));
-                    fal[i] = *(const h8v*)(sb + yswzA(row, 4 * s + 2 * hsel + 1));
-                } else {
-                    const f4 x0 = *(const f4*)(sb + yswzA(row, 4 * s + 2 * hsel));
-                    const f4 x1 = *(const f4*)(sb + yswzA(row, 4 * s + 2 * hsel + 1));
-                    split8_mix(x0, x1, fah[i], fal[i]);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int off = xswz(brow + 32 * j, 2 * s + hsel);
-                fbh[j] = *(const h8v*)(sb + ABYTES + off);
-                fbl[j] = *(const h8v*)(sb + ABYTES + BPLANE + off);
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
-                }
-        }
-    }
-
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] *= a.acc_scale;
-    const int n_base = n0 + wn * 64 + l32;
-    const int m_base = m0 + wm * 64 + 4 * hsel;
-    if (gridDim.z > 1) {
-        float* part = a.part + (int64_t)bz * a.M * a.Cout;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int m = m_base + 32 * i + 8 * (e >> 2) + (e & 3);
-                if (m >= a.M) continue;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int n = n_base + 32 * j;
-                    if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][e];
-                }
-            }
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int m = m_base + 32 * i + 8 * (e >> 2) + (e & 3);
-            if (m >= a.M) continue;
-            const int bb = m / HWo;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int n = n_base + 32 * j;
-                if (n >= a.Cout) continue;
-                float v = a.bias ? acc[i][j][e] + a.bias[n] : acc[i][j][e];
-                if (a.emb) v = v + a.emb[(int64_t)bb * a.emb_stride + n];
-                if (a.res) v = a.res[(int64_t)m * a.Cout + n] + v;
-                a.out[(int64_t)m * a.Cout + n] = v;
-            }
-        }
-}
-
-// variant ids (tools/convbench): BM x BN, wave grid, K groups
 // K1h tile width for this shape (0: K1h does not apply): the widest of 64, 32,
 // 16 dividing the image width whose 256-pixel block rows divide the height
 int conv_h_tw(const ConvArgs& a) {
@@ -950,7 +698,7 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
                 "conv_x: split-f16 forward only (variant 22: bf16)");
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_x needs channels % 32 == 0");
     CFD_REQUIRE(splits == 1 || a.part, CFD_ESTATE, "split-K needs a partial buffer");
-    {   // K1x / K1y: 32-bit buffer offsets, 24-bit pixel indices
+    {   // K1x / K1h: 32-bit buffer offsets, 24-bit pixel indices
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
         CFD_REQUIRE(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) &&
                         (int64_t)a.Cout * a.K * 2 < (1ll << 31) && a.ks * a.ks <= 9,
@@ -969,44 +717,19 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         check_launch("conv_h_kernel");
         return splits;
     }
-    if (variant == 20 || variant == 21) {   // K1h: 20 = 256-pixel blocks; 21 = 128-pixel blocks in 2 K groups
+    if (variant == 20) {   // K1h: 256-pixel blocks
         const int tw = conv_h_tw(a);
-        CFD_REQUIRE(tw > 0 && (variant == 20 || (a.Hout * a.Wout) % 128 == 0), CFD_ESHAPE,
-                    "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");
-        if (variant == 20) {
-            const dim3 g = grid(256, 128);
-            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
-            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
-            else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
-        } else {
-            const dim3 g = grid(128, 128);
-            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<128, 64, 2>), g, dim3(512), 0, st, a);
-            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<128, 32, 2>), g, dim3(512), 0, st, a);
-            else hipLaunchKernelGGL((conv_h_kernel<128, 16, 2>), g, dim3(512), 0, st, a);
-        }
+        CFD_REQUIRE(tw > 0, CFD_ESHAPE, "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");
+        const dim3 g = grid(256, 128);
+        if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
+        else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
         check_launch("conv_h_kernel");
         return splits;
     }
     switch (variant) {
-        case 0: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 2>), grid(128, 128), dim3(512), 0, st, a); break;
         case 1: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1>), grid(128, 128), dim3(256), 0, st, a); break;
         case 2: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1>), grid(256, 128), dim3(512), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((conv_x_kernel<128, 64, 2, 1, 2>), grid(128, 64), dim3(256), 0, st, a); break;
-        case 4: hipLaunchKernelGGL((conv_x_kernel<64, 128, 1, 2, 2>), grid(64, 128), dim3(256), 0, st, a); break;
-        case 5: hipLaunchKernelGGL((conv_x_kernel<64, 64, 1, 1, 4>), grid(64, 64), dim3(256), 0, st, a); break;
-        case 6: hipLaunchKernelGGL((conv_x_kernel<64, 64, 1, 1, 2>), grid(64, 64), dim3(128), 0, st, a); break;
-        case 7: hipLaunchKernelGGL((conv_x_kernel<128, 64, 2, 1, 1>), grid(128, 64), dim3(128), 0, st, a); break;
-        case 8: hipLaunchKernelGGL((conv_x_kernel<64, 128, 1, 2, 1>), grid(64, 128), dim3(128), 0, st, a); break;
-        case 9: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1, 2>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 23: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1, 2>), grid(256, 128), dim3(512), 0, st, a); break;
-        case 10: hipLaunchKernelGGL((conv_y_kernel<4>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 11: hipLaunchKernelGGL((conv_y_kernel<3>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 12: hipLaunchKernelGGL((conv_y_kernel<4, 1>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 13: hipLaunchKernelGGL((conv_y_kernel<4, 3>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 14: hipLaunchKernelGGL((conv_y_kernel<4, 5>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 15: hipLaunchKernelGGL((conv_y_kernel<4, 0, 1>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 16: hipLaunchKernelGGL((conv_y_kernel<4, 1, 1>), grid(128, 128), dim3(256), 0, st, a); break;
-        case 17: hipLaunchKernelGGL((conv_y_kernel<3, 0, 1>), grid(128, 128), dim3(256), 0, st, a); break;
         default: CFD_REQUIRE(false, CFD_EARG, "conv_x variant");
     }
     check_launch("conv_x_kernel");

@@ -870,35 +870,21 @@ struct cfd_siren {
 
 namespace {
 
-int siren_variant() {
-    static int v = [] {
-        const char* e = getenv("CFD_SIREN_VARIANT");
-        return e ? atoi(e) : 2;
-    }();
-    return v;
-}
-
+// K7 (fp32 compute): 8 waves per workgroup (the 4-wave and dual-chain variants,
+// measured slower, were removed in round 3)
 template <int NB>
 void launch_siren_nb(const cfd_siren* h, cfd::SirenArgs a, int b, hipStream_t st) {
     const int H = NB * 16;
     const size_t lds = (size_t)(2 * NB * 256 + (h->cfg.num_hidden_layers + 1) * H + 4 * H) * sizeof(float);
-    const int v = siren_variant();  // 2 (default): 8 waves/WG, 0: 4 waves/WG, 1: dual chain
-    const void* fn = v == 1 ? (const void*)cfd::siren_fused<NB, true, 4>
-                   : v == 2 ? (const void*)cfd::siren_fused<NB, false, 8>
-                            : (const void*)cfd::siren_fused<NB, false, 4>;
+    const void* fn = (const void*)cfd::siren_fused<NB, false, 8>;
     CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const int waves = v == 2 ? 8 : 4;
+    const int waves = 8;
     const int64_t tiles = cfd::ceil_div(a.N, 16 * waves);
     for (int64_t b0 = 0; b0 < b; b0 += 65535) {
         a.b0 = b0;
         const int nb = (int)std::min<int64_t>(65535, b - b0);
         const dim3 grid((unsigned)tiles, nb);
-        if (v == 1)
-            hipLaunchKernelGGL((cfd::siren_fused<NB, true, 4>), grid, dim3(256), lds, st, a);
-        else if (v == 2)
-            hipLaunchKernelGGL((cfd::siren_fused<NB, false, 8>), grid, dim3(512), lds, st, a);
-        else
-            hipLaunchKernelGGL((cfd::siren_fused<NB, false, 4>), grid, dim3(256), lds, st, a);
+        hipLaunchKernelGGL((cfd::siren_fused<NB, false, 8>), grid, dim3(512), lds, st, a);
         cfd::check_launch("siren_fused");
     }
 }

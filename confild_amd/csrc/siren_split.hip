@@ -726,25 +726,12 @@ void launch_ring(SirenArgs a, int b, hipStream_t st) {
     }
 }
 
+// K7s: 8 waves, one 16-row block per ring slot (the measured variants -- two
+// coordinate groups per wave, two blocks per slot, the scalar sine, no barrier
+// -- were removed in round 3)
 template <int NB>
 void launch_nb(SirenArgs a, int b, hipStream_t st) {
-    static const int cg = env_int("CFD_SIREN_SPLIT_CG", 1, 1, 2);
-    static const int rb = env_int("CFD_SIREN_RB", 1, 1, 2);
-    const size_t film = (size_t)(a.nh + 1) * NB * 16 + 8 * NB * 16;
-    const bool fits2 = sizeof(float) * ((size_t)2 * 2 * NB * 256 + film) <= 160 * 1024;
-    if constexpr (NB == 24) {  // timing experiment (wrong results): CFD_SIREN_NOSYNC=1
-        static const int nosync = env_int("CFD_SIREN_NOSYNC", 0, 0, 1);
-        if (nosync) return cg == 1 ? launch_ring<NB, 2, 1, 1, true>(a, b, st) : launch_ring<NB, 2, 2, 1, true>(a, b, st);
-    }
-    if constexpr (NB == 24) {  // scalar-sine variant: CFD_SIREN_PKSIN=0
-        static const int pk = env_int("CFD_SIREN_PKSIN", 1, 0, 1);
-        if (!pk && cg == 1)
-            return rb == 2 ? launch_ring<NB, 2, 1, 2, false, false>(a, b, st) : launch_ring<NB, 2, 1, 1, false, false>(a, b, st);
-    }
-    // two groups of two blocks per slot when the LDS holds them, else one block per slot
-    if (rb == 2 && fits2)
-        return cg == 1 ? launch_ring<NB, 2, 1, 2>(a, b, st) : launch_ring<NB, 2, 2, 2>(a, b, st);
-    return cg == 1 ? launch_ring<NB, 2, 1, 1>(a, b, st) : launch_ring<NB, 2, 2, 1>(a, b, st);
+    launch_ring<NB, 2, 1, 1>(a, b, st);
 }
 }  // namespace
 
@@ -772,47 +759,20 @@ bool siren_split32_supported(int H, int nh) {
            sizeof(float) * ((size_t)4 * (H / 32) * 512 + film) <= 160 * 1024;
 }
 
+// HWSIN 4 (default): weights pre-scaled by w0/2pi, v_sin_f32 on the revolutions;
+// 3 (CFD_SIREN_HWSIN=3): the same after an explicit fract.  The radian-domain
+// sines (0: polynomial, 1: 2pi Cody-Waite, 2: reduction in revolutions) stay
+// in the sine probe (cfd_sine_probe) and the K7s/K9d kernels; their full
+// decoder instantiations and the timing experiments were removed in round 3.
 void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
-    static const int hw = env_int("CFD_SIREN_HWSIN", 4, 0, 4);
-    if (hw >= 3) {
-        CFD_REQUIRE(a.wimg_rev && a.wrev, CFD_EARG, "split32 revolution image not set");
-        a.wimg = a.wimg_rev;
-        switch (H) {
-            case 64: return hw == 3 ? launch_split32<2, 0, 3>(a, b, st) : launch_split32<2, 0, 4>(a, b, st);
-            case 128: return hw == 3 ? launch_split32<4, 0, 3>(a, b, st) : launch_split32<4, 0, 4>(a, b, st);
-            case 256: return hw == 3 ? launch_split32<8, 0, 3>(a, b, st) : launch_split32<8, 0, 4>(a, b, st);
-            case 384: {
-                static const int exp = env_int("CFD_SIREN_EXP", 0, 0, 4);
-                if (hw == 4 && exp == 4) return launch_split32<12, 4, 4>(a, b, st);   // timing experiment
-                if (hw == 4 && exp == 1) return launch_split32<12, 1, 4>(a, b, st);   // timing experiment
-                return hw == 3 ? launch_split32<12, 0, 3>(a, b, st) : launch_split32<12, 0, 4>(a, b, st);
-            }
-            default: break;
-        }
-    }
-    if (hw) {
-        switch (H) {
-            case 64: return hw == 2 ? launch_split32<2, 0, 2>(a, b, st) : launch_split32<2, 0, 1>(a, b, st);
-            case 128: return hw == 2 ? launch_split32<4, 0, 2>(a, b, st) : launch_split32<4, 0, 1>(a, b, st);
-            case 256: return hw == 2 ? launch_split32<8, 0, 2>(a, b, st) : launch_split32<8, 0, 1>(a, b, st);
-            case 384: return hw == 2 ? launch_split32<12, 0, 2>(a, b, st) : launch_split32<12, 0, 1>(a, b, st);
-            default: break;
-        }
-    }
+    static const int hw = env_int("CFD_SIREN_HWSIN", 4, 3, 4);
+    CFD_REQUIRE(a.wimg_rev && a.wrev, CFD_EARG, "split32 revolution image not set");
+    a.wimg = a.wimg_rev;
     switch (H) {
-        case 64: return launch_split32<2>(a, b, st);
-        case 128: return launch_split32<4>(a, b, st);
-        case 256: return launch_split32<8>(a, b, st);
-        case 384: {
-            static const int exp = env_int("CFD_SIREN_EXP", 0, 0, 4);
-            switch (exp) {
-                case 1: return launch_split32<12, 1>(a, b, st);
-                case 2: return launch_split32<12, 2>(a, b, st);
-                case 3: return launch_split32<12, 3>(a, b, st);
-                case 4: return launch_split32<12, 4>(a, b, st);
-                default: return launch_split32<12>(a, b, st);
-            }
-        }
+        case 64: return hw == 3 ? launch_split32<2, 0, 3>(a, b, st) : launch_split32<2, 0, 4>(a, b, st);
+        case 128: return hw == 3 ? launch_split32<4, 0, 3>(a, b, st) : launch_split32<4, 0, 4>(a, b, st);
+        case 256: return hw == 3 ? launch_split32<8, 0, 3>(a, b, st) : launch_split32<8, 0, 4>(a, b, st);
+        case 384: return hw == 3 ? launch_split32<12, 0, 3>(a, b, st) : launch_split32<12, 0, 4>(a, b, st);
         default: throw Error{CFD_EARG, "32x32 split-f16 SIREN needs hidden_features in {64, 128, 256, 384}"};
     }
 }

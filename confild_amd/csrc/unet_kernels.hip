@@ -90,11 +90,21 @@ __global__ __launch_bounds__(1024) void gn_finalize_kernel(GnArgs a) {
     __shared__ double red[2][1024];
     const int grp = threadIdx.x >> 5, sub = threadIdx.x & 31;
     {
+        // every 32nd chunk, four loads in flight, added in chunk order
         double s = 0, s2 = 0;
-        for (int ch = sub; ch < a.nchunks; ch += 32) {
-            const double* src = a.part + ((b * a.nchunks + ch) * 32 + grp) * 2;
-            s += src[0];
-            s2 += src[1];
+        for (int ch = sub; ch < a.nchunks; ch += 128) {
+            double2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = ch + 32 * u;
+                v[u] = c < a.nchunks ? *(const double2*)(a.part + ((b * a.nchunks + c) * 32 + grp) * 2)
+                                     : double2{0.0, 0.0};
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s += v[u].x;
+                s2 += v[u].y;
+            }
         }
         red[0][threadIdx.x] = s;
         red[1][threadIdx.x] = s2;
@@ -1446,178 +1456,6 @@ __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, c
     }
 }
 
-// K4s2: the same split attention with K and V staged per 32-key block in LDS by
-// the workgroup (each thread fetches one K row-chunk and one V column of the
-// block from qkv, scales K, splits to hi/lo f16 and writes the fragment layouts
-// attn_kv_split would produce), double-buffered: the four waves share one copy
-// instead of each loading the fragments from L2, the next block's fetch overlaps
-// this block's MFMAs, and the separate pack kernel (and its HBM round trip) is
-// gone.  The fragments, the MFMA order and the softmax are those of
-// attention_split_kernel, so the output is bit-identical to it.
-template <int CH>
-__global__ __launch_bounds__(256) void attention_lds_kernel(AttnArgs a) {
-    constexpr int NJ = CH / 32, ND = CH / 16;
-    constexpr int KFR = 2 * NJ * 128, VFR = ND * 128;   // h8v per stage: K (2 key tiles), V
-    constexpr int PK = (4 * CH + 255) / 256;            // (key, 8-channel chunk) / (channel, key group) pairs per thread
-    __shared__ h8v kv[2][KFR + VFR];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g = lane >> 4, li = lane & 15;
-    const int h = blockIdx.y;
-    const int64_t b = blockIdx.z;
-    const int T = a.T, T32 = (T + 31) / 32 * 32;
-    const int q0 = blockIdx.x * 64 + wave * 16;
-    const bool active = q0 < T;   // wave-uniform; inactive waves still stage and sync
-    const int C3 = 3 * a.C;
-    const float* base = a.qkv + b * (int64_t)T * C3 + (int64_t)h * 3 * CH;
-    CFD_DASSERT(h * CH + CH <= a.C);
-
-    float kr[PK][8], vr[PK][8];
-    auto fetch = [&](int kb) {
-#pragma unroll
-        for (int e = 0; e < PK; ++e) {
-            const int pidx = tid + 256 * e;
-            if (pidx < 4 * CH) {
-                {   // K: key k, channels 8 c8 .. +8
-                    const int c8 = pidx % (CH / 8), k = pidx / (CH / 8);
-                    const int key = kb + k;
-                    const float* kp = base + (int64_t)min(key, T - 1) * C3 + CH + 8 * c8;
-                    const f4 v0 = *(const f4*)kp, v1 = *(const f4*)(kp + 4);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        kr[e][t] = key < T ? v0[t] * kln2(a.scale) : 0.f;
-                        kr[e][4 + t] = key < T ? v1[t] * kln2(a.scale) : 0.f;
-                    }
-                }
-                {   // V: channel ci, keys kmap(gg, 0..7)
-                    const int ci = pidx % CH, gg = pidx / CH;
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const int key = kb + (t < 4 ? 4 * gg + t : 16 + 4 * gg + t - 4);
-                        vr[e][t] = key < T ? base[(int64_t)key * C3 + 2 * CH + ci] : 0.f;
-                    }
-                }
-            }
-        }
-    };
-    auto stage = [&](int buf) {
-#pragma unroll
-        for (int e = 0; e < PK; ++e) {
-            const int pidx = tid + 256 * e;
-            if (pidx < 4 * CH) {
-                h8v hi, lo;
-                {
-                    const int c8 = pidx % (CH / 8), k = pidx / (CH / 8);
-                    split8_f16(kr[e], hi, lo);
-                    const int o = ((k >> 4) * NJ + (c8 >> 2)) * 128 + (k & 15) + 16 * (c8 & 3);
-                    kv[buf][o] = hi;
-                    kv[buf][o + 64] = lo;
-                }
-                {
-                    const int ci = pidx % CH, gg = pidx / CH;
-                    split8_f16(vr[e], hi, lo);
-                    const int o = KFR + (ci >> 4) * 128 + (ci & 15) + 16 * gg;
-                    kv[buf][o] = hi;
-                    kv[buf][o + 64] = lo;
-                }
-            }
-        }
-    };
-
-    h8v qh[NJ], ql[NJ];
-    {
-        const int tq = min(q0 + li, T - 1);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const float* qp = base + (int64_t)tq * C3 + 32 * j + 8 * g;
-            float v[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) v[t] = qp[t] * a.scale;
-            split8_f16(v, qh[j], ql[j]);
-        }
-    }
-    f4 O[ND];
-#pragma unroll
-    for (int d = 0; d < ND; ++d) O[d] = f4{0.f, 0.f, 0.f, 0.f};
-    float mrun = -INFINITY, lrun = 0.f;
-
-    fetch(0);
-    stage(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kb = 0; kb < T32; kb += 32) {
-        const bool more = kb + 32 < T32;
-        if (more) fetch(kb + 32);
-        if (active) {
-            const h8v* kp0 = kv[cur] + lane;
-            f4 st[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                st[u] = f4{0.f, 0.f, 0.f, 0.f};
-                const h8v* kp = kp0 + u * NJ * 128;
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    const h8v kh = kp[j * 128], kl = kp[j * 128 + 64];
-                    st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qh[j], st[u], 0, 0, 0);
-                    st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, ql[j], st[u], 0, 0, 0);
-                    st[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[j], st[u], 0, 0, 0);
-                }
-            }
-            float mx = -INFINITY;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if (kb + 16 * u + 4 * g + r >= T) st[u][r] = -INFINITY;
-                    mx = fmaxf(mx, st[u][r]);
-                }
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
-            const float mnew = fmaxf(mrun, mx);
-            const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
-            float p[8], ps = 0.f;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    p[4 * u + r] = __builtin_amdgcn_exp2f(st[u][r] - mnew);
-                    ps += p[4 * u + r];
-                }
-            ps += __shfl_xor(ps, 16);
-            ps += __shfl_xor(ps, 32);
-            lrun = lrun * alpha + ps;
-            mrun = mnew;
-#pragma unroll
-            for (int d = 0; d < ND; ++d) O[d] = O[d] * alpha;
-            h8v ph, pl;
-            split8_f16(p, ph, pl);
-            const h8v* vp = kv[cur] + KFR + lane;
-#pragma unroll
-            for (int d = 0; d < ND; ++d) {
-                const h8v vh = vp[d * 128], vl = vp[d * 128 + 64];
-                O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, O[d], 0, 0, 0);
-                O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, O[d], 0, 0, 0);
-                O[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, O[d], 0, 0, 0);
-            }
-        }
-        if (more) stage(cur ^ 1);
-        __syncthreads();
-        cur ^= 1;
-    }
-    if (!active) return;
-    const int tq = q0 + li;
-    if (a.lse && g == 0 && tq < T)
-        a.lse[((int64_t)b * gridDim.y + h) * T + tq] = (mrun + log2f(lrun)) * 0.69314718055994530942f;
-    if (tq < T) {
-        float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
-        const float inv = 1.0f / lrun;
-#pragma unroll
-        for (int d = 0; d < ND; ++d) {
-            f4 v = O[d] * inv;
-            *(f4*)(op + 16 * d + 4 * g) = v;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // K5: timestep embedding and small dense layers.
 // ---------------------------------------------------------------------------
@@ -1995,21 +1833,6 @@ size_t attention_split_floats(int T, int C) { return (size_t)(T + 31) / 32 * 32 
 
 void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st) {
     CFD_REQUIRE(CH == 32 || CH == 64 || CH == 128, CFD_ESHAPE, "split attention needs head channels 32, 64 or 128");
-    // K4s2 (CFD_ATTN_LDS=1): K/V staged in LDS per workgroup, no pack kernel;
-    // bit-identical, measured slower at config B (U-Net 4.47 -> 4.56 ms same-box:
-    // 129 registers cost a wave per SIMD and the per-block barrier binds the
-    // four waves), so off
-    static const int lds = env_int("CFD_ATTN_LDS", 0);
-    if (lds) {
-        const dim3 grid((unsigned)ceil_div(a.T, 64), heads, B);
-        switch (CH) {
-            case 32: hipLaunchKernelGGL(attention_lds_kernel<32>, grid, dim3(256), 0, st, a); break;
-            case 64: hipLaunchKernelGGL(attention_lds_kernel<64>, grid, dim3(256), 0, st, a); break;
-            default: hipLaunchKernelGGL(attention_lds_kernel<128>, grid, dim3(256), 0, st, a); break;
-        }
-        check_launch("attention_lds_kernel");
-        return;
-    }
     const int T32 = (a.T + 31) / 32 * 32;
     h8v* kf = (h8v*)kvws;
     h8v* vf = kf + (size_t)B * heads * (T32 / 16) * (CH / 32) * 128;
@@ -2036,23 +1859,14 @@ void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* 
         check_launch("attention_dma_kernel");
         return;
     }
-    // CFD_ATTN_QT=2: two query tiles per wave where that still leaves >= 256
-    // workgroups (per sample: the choice must not depend on the batch).  Measured
-    // slower (U-Net 4.48 -> 4.62 ms same-box: 181 registers halve the waves per
-    // SIMD, which costs more than the halved fragment traffic saves); off
-    static const int qt_env = env_int("CFD_ATTN_QT", 1);
-    const int qt = qt_env >= 2 && (int64_t)ceil_div(a.T, 128) * heads * 8 >= 256 ? 2 : 1;
-    const dim3 grid((unsigned)ceil_div(a.T, 64 * qt), heads, B);
-    if (qt == 1) switch (CH) {
+    // K4s (CFD_ATTN_DMA=0): every wave streams its (sample, head)'s fragments from
+    // L2 (K4s2, K/V staged per block in LDS without a pack kernel, and two query
+    // tiles per wave measured slower and were removed in round 3)
+    const dim3 grid((unsigned)ceil_div(a.T, 64), heads, B);
+    switch (CH) {
         case 32: hipLaunchKernelGGL((attention_split_kernel<32, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
         case 64: hipLaunchKernelGGL((attention_split_kernel<64, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
         case 128: hipLaunchKernelGGL((attention_split_kernel<128, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
-        default: throw Error{CFD_ESHAPE, "split attention head channels must be 32, 64 or 128"};
-    }
-    else switch (CH) {
-        case 32: hipLaunchKernelGGL((attention_split_kernel<32, 2>), grid, dim3(256), 0, st, a, kf, vf); break;
-        case 64: hipLaunchKernelGGL((attention_split_kernel<64, 2>), grid, dim3(256), 0, st, a, kf, vf); break;
-        case 128: hipLaunchKernelGGL((attention_split_kernel<128, 2>), grid, dim3(256), 0, st, a, kf, vf); break;
         default: throw Error{CFD_ESHAPE, "split attention head channels must be 32, 64 or 128"};
     }
     check_launch("attention_split_kernel");

@@ -1,5 +1,5 @@
 """Development check: the U-Net forward under two environments (child processes)
-must be bit-identical (e.g. CFD_ATTN_LDS=0 vs 1).  Usage: attn_bitcheck.py ENV_A ENV_B"""
+must be bit-identical (e.g. CFD_ATTN_DMA=0 vs 1).  Usage: attn_bitcheck.py ENV_A ENV_B"""
 import os
 import subprocess
 import sys
