@@ -288,7 +288,26 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
             const int p = r0 + k * rows;
             v[k] = act && p < HW ? *(const f4*)(kpart + ib + k * istep) : f4{0.f, 0.f, 0.f, 0.f};
         }
-        for (int sp = 1; sp < a.ksplits; ++sp) {
+        // UN slabs' loads in flight per round (one slab per round waited one
+        // memory latency per split: 16 at the 8^2 level), added in split order
+        constexpr int UN = IPT <= 2 ? 4 : IPT <= 4 ? 2 : 1;
+        int sp = 1;
+        for (; sp + UN - 1 < a.ksplits; sp += UN) {
+            f4 u[UN][IPT];
+#pragma unroll
+            for (int q2 = 0; q2 < UN; ++q2)
+#pragma unroll
+                for (int k = 0; k < IPT; ++k) {
+                    const int p = r0 + k * rows;
+                    u[q2][k] = act && p < HW ? *(const f4*)(kpart + (sp + q2) * slab + ib + k * istep)
+                                             : f4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+            for (int q2 = 0; q2 < UN; ++q2)
+#pragma unroll
+                for (int k = 0; k < IPT; ++k) v[k] += u[q2][k];
+        }
+        for (; sp < a.ksplits; ++sp) {
 #pragma unroll
             for (int k = 0; k < IPT; ++k) {
                 const int p = r0 + k * rows;
@@ -858,8 +877,18 @@ __global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
     const int64_t total4 = (int64_t)a.M * a.Cout / 4;
     if (i4 >= total4) return;
     const int64_t i = i4 * 4;
+    const int64_t slab = (int64_t)a.M * a.Cout;
     f4 s = *(const f4*)(a.part + i);
-    for (int k = 1; k < splits; ++k) s += *(const f4*)(a.part + (int64_t)k * a.M * a.Cout + i);
+    int k = 1;
+    for (; k + 3 < splits; k += 4) {   // four slabs' loads in flight, added in split order
+        const f4 u0 = *(const f4*)(a.part + k * slab + i), u1 = *(const f4*)(a.part + (k + 1) * slab + i);
+        const f4 u2 = *(const f4*)(a.part + (k + 2) * slab + i), u3 = *(const f4*)(a.part + (k + 3) * slab + i);
+        s += u0;
+        s += u1;
+        s += u2;
+        s += u3;
+    }
+    for (; k < splits; ++k) s += *(const f4*)(a.part + k * slab + i);
     const int64_t m = i / a.Cout;
     const int n = (int)(i - m * a.Cout);
     const int bb = (int)(m / (a.Hout * a.Wout));
