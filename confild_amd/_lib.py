@@ -101,6 +101,12 @@ _SIGS = {
                                          C.c_size_t, C.c_void_p]),
     "cfd_siren_tape_vjp": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
                                      C.c_int64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "cfd_siren_train_workspace_bytes": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_size_t)]),
+    "cfd_siren_train_grad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
+                                       C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_size_t, C.c_void_p]),
+    "cfd_adam_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_double, C.c_double,
+                                C.c_double, C.c_double, C.c_int64, C.c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -329,6 +329,226 @@ __global__ __launch_bounds__(256) void sensor_sum_kernel(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// K10: CNF autodecoder training step (N/scripts/train.py:392-416, MSELoss): the
+// gradients of mean((SIREN(coords, z_rows) - target)^2) w.r.t. every net1 / net2
+// parameter and the batch's latent rows, from the DPS tape (pre-activations u_i
+// and deltas delta_i per (row, coordinate) pair, siren_tape_fwd / _bwd below).
+// Every weight gradient is a "TN" product over the pairs, C[m, n] = sum_k
+// X[k, m] Y[k, n] with both operands pair-major (k = pair): X a delta slice,
+// Y the previous layer's activation sin(w0 u) recomputed from the tape with the
+// forward's own sine (so it is the activation the forward used, bit for bit).
+// fp32 MFMA 16x16x4 (exact products), split over k in a fixed slicing and the
+// slices added in order: deterministic and independent of the launch.
+// ---------------------------------------------------------------------------
+
+// gout = scale * (out - target) (MSELoss 'mean' backward, scale = 2 / numel as
+// ATen's mse_loss_backward forms it); per-block sums of (out - target)^2 in double
+__global__ __launch_bounds__(256) void mse_grad_kernel(const float* __restrict__ out, const float* __restrict__ target,
+                                                       float* __restrict__ gout, int64_t n, float scale,
+                                                       double* __restrict__ part) {
+    __shared__ double red[256];
+    double s = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float d = out[i] - target[i];
+        gout[i] = d * scale;
+        s += (double)d * d;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// *sse += sum of the block partials, in block order
+__global__ void sse_accum_kernel(const double* __restrict__ part, int nb, float* sse) {
+    if (threadIdx.x != 0) return;
+    double s = 0;
+    for (int i = 0; i < nb; ++i) s += part[i];
+    *sse += (float)s;
+}
+
+// TN product slice: C[z] (M x N) = sum_{k in slice z} X[k * ldx + m] * f(Y[row(k) * ldy + n]),
+// row(k) = k % ymod (ymod > 0: the coordinate of pair k) else k; f by YF:
+// 0 identity, 1 sin(w0 y) (sin_cw: the tape forward's sine), 2 one (column sums).
+// T x T output tiles (T = 64 or 128) over 4 waves (2 x 2, (T/2)^2 each), 16-deep
+// k steps staged through LDS, the next step's operands loaded into registers
+// while this step's MFMAs run.
+template <int YF, int T>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ X, int64_t ldx,
+                                                      const float* __restrict__ Y, int64_t ldy, int64_t ymod,
+                                                      float w0f, float* __restrict__ C, int M, int N, int64_t K,
+                                                      int64_t kspan) {
+    constexpr int WT = T / 2, NBK = WT / 16;        // wave tile, 16x16 blocks per wave side
+    constexpr int PASS = T / 64;                    // (16 x T) tile = PASS x 256 threads x 4 values
+    __shared__ float Xs[16][T + 4];
+    __shared__ float Ys[16][T + 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.y * T, n0 = blockIdx.x * T;
+    const int64_t kbeg = (int64_t)blockIdx.z * kspan, kend = min(K, kbeg + kspan);
+    f4 acc[NBK][NBK];
+#pragma unroll
+    for (int i = 0; i < NBK; ++i)
+#pragma unroll
+        for (int j = 0; j < NBK; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    float xr[PASS][4], yr[PASS][4];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int ps = 0; ps < PASS; ++ps) {
+            const int e = tid + ps * 256;
+            const int kr = e / (T / 4), c4 = (e % (T / 4)) * 4;
+            const int64_t k = k0 + kr;
+            const bool kin = k < kend;
+            const int64_t yrow = ymod > 0 ? k % ymod : k;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int m = m0 + c4 + j, n = n0 + c4 + j;
+                xr[ps][j] = kin && m < M ? X[k * ldx + m] : 0.f;
+                float y = 0.f;
+                if (kin && n < N) {
+                    if constexpr (YF == 2) y = 1.f;
+                    else y = Y[yrow * ldy + n];
+                }
+                yr[ps][j] = y;
+            }
+        }
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (int ps = 0; ps < PASS; ++ps) {
+            const int e = tid + ps * 256;
+            const int kr = e / (T / 4), c4 = (e % (T / 4)) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                Xs[kr][c4 + j] = xr[ps][j];
+                float y = yr[ps][j];
+                if constexpr (YF == 1) y = sin_cw(w0f * y);   // padding: sin(0) = 0 (and X is zero there)
+                Ys[kr][c4 + j] = y;
+            }
+        }
+    };
+    if (kbeg < kend) load(kbeg);
+    for (int64_t k0 = kbeg; k0 < kend; k0 += 16) {
+        stage();
+        __syncthreads();
+        if (k0 + 16 < kend) load(k0 + 16);
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 4) {
+            float fa[NBK], fb[NBK];
+#pragma unroll
+            for (int i = 0; i < NBK; ++i) fa[i] = Xs[kk + (lane >> 4)][wm * WT + 16 * i + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < NBK; ++j) fb[j] = Ys[kk + (lane >> 4)][wn * WT + 16 * j + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < NBK; ++i)
+#pragma unroll
+                for (int j = 0; j < NBK; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    float* Cz = C + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int i = 0; i < NBK; ++i)
+#pragma unroll
+        for (int j = 0; j < NBK; ++j) {
+            const int n = n0 + wn * WT + 16 * j + (lane & 15);
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * WT + 16 * i + 4 * (lane >> 4) + r;
+                if (m < M) Cz[(int64_t)m * N + n] = acc[i][j][r];
+            }
+        }
+}
+
+// G[m * N + n] += sum over the slices of part[z][m, n], z in order (torch's
+// gradient accumulation: param.grad + this backward's gradient)
+__global__ __launch_bounds__(256) void tn_accum_kernel(const float* __restrict__ part, int64_t MN, int splits,
+                                                       float* __restrict__ G) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= MN) return;
+    float s = part[i];
+    for (int z = 1; z < splits; ++z) s += part[z * MN + i];
+    G[i] = G[i] + s;
+}
+
+// zr (R, L) = Z[rows[r]] (the batch's latent rows, LatentContainer.forward)
+__global__ void gather_rows_kernel(const float* __restrict__ Z, const int64_t* __restrict__ rows, float* __restrict__ zr,
+                                   int R, int L) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)R * L) return;
+    const int64_t r = i / L, l = i - r * L;
+    zr[i] = Z[rows[r] * L + l];
+}
+
+// G[rows[r]] += g[r] (distinct rows: the host checks)
+__global__ void scatter_add_rows_kernel(const float* __restrict__ g, const int64_t* __restrict__ rows,
+                                        float* __restrict__ G, int R, int L) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)R * L) return;
+    const int64_t r = i / L, l = i - r * L;
+    float* dst = G + rows[r] * L + l;
+    *dst = *dst + g[i];
+}
+
+// Per-row sums over the coordinates, D[r, f] = sum_s delta[(r Ns + s) nf + f], as
+// slice partials: part[z][r][f] over coordinates [z span, (z+1) span) -- every
+// thread one column, rows read coalesced (the one-thread-per-column loop over
+// all Ns coordinates, sensor_sum_kernel, waited one load per coordinate: 24.6 ms
+// for a Case4-width batch of 4 x 65536 pairs).  tn_accum_kernel adds the slices
+// in order.
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ delta, float* __restrict__ part,
+                                                          int64_t Ns, int64_t nf, int R, int64_t span) {
+    const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int r = blockIdx.y, z = blockIdx.z;
+    if (f >= nf) return;
+    const int64_t s0 = z * span, s1 = min(Ns, s0 + span);
+    const float* src = delta + ((int64_t)r * Ns) * nf + f;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;   // four rows in flight, added in row order below
+    int64_t s = s0;
+    for (; s + 3 < s1; s += 4) {
+        const float v0 = src[s * nf], v1 = src[(s + 1) * nf], v2 = src[(s + 2) * nf], v3 = src[(s + 3) * nf];
+        a0 += v0;
+        a1 += v1;
+        a2 += v2;
+        a3 += v3;
+    }
+    for (; s < s1; ++s) a0 += src[s * nf];
+    part[((int64_t)z * R + r) * nf + f] = (a0 + a1) + (a2 + a3);
+}
+
+// k-slices of a TN product: a function of K only (fixed slicing, deterministic)
+static int64_t tn_kspan(int64_t K) {
+    const int64_t span = std::max<int64_t>(256, (K + 63) / 64);
+    return (span + 15) / 16 * 16;
+}
+
+// G (M x N) += TN(X, Y) over K rows; part: scratch of tn_splits * M * N floats
+template <int YF>
+static void launch_tn(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t ymod, float w0f, float* G,
+                      int M, int N, int64_t K, float* part, hipStream_t st) {
+    const int64_t span = tn_kspan(K);
+    const int splits = (int)((K + span - 1) / span);
+    if (M >= 128 && N >= 128) {   // the hidden-layer weight gradients: 128 x 128 tiles
+        const dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(M, 128), (unsigned)splits);
+        hipLaunchKernelGGL((gemm_tn_kernel<YF, 128>), grid, dim3(256), 0, st, X, ldx, Y, ldy, ymod, w0f, part, M, N,
+                           K, span);
+    } else {
+        const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(M, 64), (unsigned)splits);
+        hipLaunchKernelGGL((gemm_tn_kernel<YF, 64>), grid, dim3(256), 0, st, X, ldx, Y, ldy, ymod, w0f, part, M, N,
+                           K, span);
+    }
+    check_launch("gemm_tn_kernel");
+    const int64_t MN = (int64_t)M * N;
+    hipLaunchKernelGGL(tn_accum_kernel, dim3((unsigned)ceil_div(MN, 256)), dim3(256), 0, st, part, MN, splits, G);
+    check_launch("tn_accum_kernel");
+}
+
+// ---------------------------------------------------------------------------
 // Latent gradient (DPS adjoint): d<g, A(z)>/dz for the
 // Case4 measurement operator A = y_norm.denormalize(SIREN(x_norm(sensors), z))
 // (measurements.py:219-226).  The P = R x Ns (latent row, sensor) pairs are the
@@ -1376,6 +1596,150 @@ extern "C" int cfd_siren_tape_vjp(cfd_siren* h, const float* g_out, int64_t Ns, 
             hipLaunchKernelGGL(cfd::siren_latent_grad, dim3(R), dim3(256), lds, st, a.delta, h->V, g_latents,
                                (int)Ns, nh + 1, H, L);
             cfd::check_launch("siren_latent_grad");
+        }
+    });
+}
+
+// ---------------------------------------------------------------------------
+// K10 C ABI: one backward of the CNF autodecoder training loop.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct TrainWs {
+    float *film, *u, *delta, *D, *gpart, *zr, *out, *gout, *gz, *tpart;
+    double* sse;
+    size_t floats;
+};
+
+constexpr int kSseBlocks = 1024;
+
+TrainWs train_ws(const cfd_siren* h, int64_t N, int R, void* base) {
+    const size_t nl = h->cfg.num_hidden_layers + 1, H = h->cfg.hidden_features, L = h->cfg.in_latent_features;
+    const size_t c = h->cfg.out_features, d = h->cfg.in_coord_features, nf = nl * H, P = (size_t)R * N;
+    float* p = (float*)base;
+    size_t off = 0;
+    auto take = [&](size_t n) {
+        float* q = p ? p + off : nullptr;
+        off += (n + 63) / 64 * 64;
+        return q;
+    };
+    TrainWs w{};
+    // film, u, delta, D back to back: the layout tape_args / the DPS latent gradient use
+    w.film = take((size_t)R * nf);
+    w.u = p ? w.film + (size_t)R * nf : nullptr;
+    off += 2 * P * nf;
+    w.delta = p ? w.u + P * nf : nullptr;
+    off = (off + 63) / 64 * 64;
+    w.D = take((size_t)R * nf);
+    w.gpart = take((size_t)cfd::gemm_splits((int)nf) * R * L);
+    w.zr = take((size_t)R * L);
+    w.out = take(P * c);
+    w.gout = take(P * c);
+    w.gz = take((size_t)R * L);
+    w.sse = (double*)take(2 * kSseBlocks);
+    // TN-product slices (<= 64 of the largest gradient) and the column-sum slices (<= 64 x R x nf)
+    w.tpart = take((size_t)64 * std::max(std::max(std::max(H * H, H * L), std::max(H * d, c * H)), (size_t)R * nf));
+    w.floats = off;
+    return w;
+}
+
+}  // namespace
+
+extern "C" int cfd_siren_train_workspace_bytes(const cfd_siren* h, int64_t N, int R, size_t* bytes) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && bytes && N >= 0 && R >= 0, CFD_EARG, "bad argument");
+        *bytes = sizeof(float) * train_ws(h, N, R, nullptr).floats;
+    });
+}
+
+extern "C" int cfd_siren_train_grad(cfd_siren* h, const float* coords, int64_t N, const float* latents,
+                                    const int64_t* rows, int R, const float* target, float scale, float* grad,
+                                    float* grad_latents, float* sse, void* ws, size_t ws_bytes, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && coords && latents && rows && target && grad && grad_latents && sse && ws, CFD_EARG,
+                    "null argument");
+        CFD_REQUIRE(N >= 1 && N <= (1 << 20) && R >= 1, CFD_EARG, "bad coordinate / row count");
+        CFD_REQUIRE(((uintptr_t)ws & 15) == 0, CFD_EARG, "workspace must be 16-byte aligned");
+        for (const auto& p : h->params) CFD_REQUIRE(p.set, CFD_ESTATE, "SIREN parameter not set: " + p.key);
+        const TrainWs w = train_ws(h, N, R, ws);
+        CFD_REQUIRE(ws_bytes >= sizeof(float) * w.floats, CFD_EARG, "workspace too small");
+        const int nh = h->cfg.num_hidden_layers, H = h->cfg.hidden_features, L = h->cfg.in_latent_features;
+        const int c = h->cfg.out_features, d = h->cfg.in_coord_features;
+        const int64_t nf = (int64_t)(nh + 1) * H, P = (int64_t)R * N;
+        const float w0f = h->cfg.w0;
+        auto st = (hipStream_t)stream;
+        // parameter offsets in the flat gradient (cfd_siren_param_info order, reference shapes)
+        std::vector<size_t> off;
+        size_t o = 0;
+        for (const auto& p : h->params) {
+            off.push_back(o);
+            size_t n = 1;
+            for (auto e : p.shape) n *= (size_t)e;
+            o += n;
+        }
+        auto goff = [&](const std::string& key) -> float* {
+            for (size_t i = 0; i < h->params.size(); ++i)
+                if (h->params[i].key == key) return grad + off[i];
+            throw cfd::Error{CFD_ESTATE, "internal: no parameter " + key};
+        };
+        // forward with tape (LatentContainer rows -> FiLM -> siren_tape_fwd), raw in and out
+        hipLaunchKernelGGL(cfd::gather_rows_kernel, dim3((unsigned)cfd::ceil_div((int64_t)R * L, 256)), dim3(256), 0,
+                           st, latents, rows, w.zr, R, L);
+        cfd::check_launch("gather_rows_kernel");
+        film_vectors(h, w.zr, R, w.film, st);
+        cfd::SirenTapeArgs a{};
+        tape_args(h, a, N, R, ws);
+        a.coords = coords;
+        a.out = w.out;
+        launch_tape(h, a, false, st);
+        // loss gradient and sum of squared errors
+        const int nb = (int)std::min<int64_t>(kSseBlocks, cfd::ceil_div(P * c, 256));
+        hipLaunchKernelGGL(cfd::mse_grad_kernel, dim3(nb), dim3(256), 0, st, w.out, target, w.gout, P * c, scale, w.sse);
+        cfd::check_launch("mse_grad_kernel");
+        hipLaunchKernelGGL(cfd::sse_accum_kernel, dim3(1), dim3(64), 0, st, w.sse, nb, sse);
+        cfd::check_launch("sse_accum_kernel");
+        // backward through the chain: every delta_i (P, nl, H)
+        a.gout = w.gout;
+        launch_tape(h, a, true, st);
+        // per-row sums D_i[r] = sum over the coordinates of delta_i = dL/dF_i[r]
+        {
+            const int64_t span = cfd::tn_kspan(N);
+            const int slices = (int)((N + span - 1) / span);
+            float* part = slices > 1 ? w.tpart : w.D;
+            hipLaunchKernelGGL(cfd::colsum_part_kernel, dim3((unsigned)cfd::ceil_div(nf, 256), R, slices), dim3(256),
+                               0, st, w.delta, part, N, nf, R, span);
+            cfd::check_launch("colsum_part_kernel");
+            if (slices > 1) {
+                CFD_HIP(hipMemsetAsync(w.D, 0, sizeof(float) * R * nf, st));
+                hipLaunchKernelGGL(cfd::tn_accum_kernel, dim3((unsigned)cfd::ceil_div(R * nf, 256)), dim3(256), 0, st,
+                                   part, R * nf, slices, w.D);
+                cfd::check_launch("tn_accum_kernel");
+            }
+        }
+        // latent rows: g_z = sum_i D_i V_i, added into grad_latents[rows]
+        if (L % 4 == 0 && nf % 16 == 0) {
+            cfd::launch_gemm_f32(false, w.D, (int)nf, h->V, L, nullptr, w.gz, L, R, L, (int)nf, st, w.gpart);
+        } else {
+            CFD_REQUIRE(false, CFD_ESHAPE, "training needs in_latent_features % 4 == 0 and (nh+1)*H % 16 == 0");
+        }
+        hipLaunchKernelGGL(cfd::scatter_add_rows_kernel, dim3((unsigned)cfd::ceil_div((int64_t)R * L, 256)),
+                           dim3(256), 0, st, w.gz, rows, grad_latents, R, L);
+        cfd::check_launch("scatter_add_rows_kernel");
+        // weights: dW_0 = delta_0^T coords, dW_i = delta_i^T sin(w0 u_{i-1}), dW_out = g^T sin(w0 u_nh)
+        cfd::launch_tn<0>(w.delta, nf, coords, d, N, w0f, goff("net1.0.weight"), H, d, P, w.tpart, st);
+        for (int i = 1; i <= nh; ++i)
+            cfd::launch_tn<1>(w.delta + (int64_t)i * H, nf, w.u + (int64_t)(i - 1) * H, nf, 0, w0f,
+                              goff("net1." + std::to_string(i) + ".weight"), H, H, P, w.tpart, st);
+        const std::string lo = "net1." + std::to_string(nh + 1);
+        cfd::launch_tn<1>(w.gout, c, w.u + (int64_t)nh * H, nf, 0, w0f, goff(lo + ".weight"), c, H, P, w.tpart, st);
+        cfd::launch_tn<2>(w.gout, c, nullptr, 0, 0, w0f, goff(lo + ".bias"), c, 1, P, w.tpart, st);
+        // FiLM side: db_i = sum_r D_i[r], dV_i = D_i^T z
+        for (int i = 0; i <= nh; ++i) {
+            const std::string k = std::to_string(i);
+            cfd::launch_tn<2>(w.D + (int64_t)i * H, nf, nullptr, 0, 0, w0f, goff("net1." + k + ".bias"), H, 1, R,
+                              w.tpart, st);
+            cfd::launch_tn<0>(w.D + (int64_t)i * H, nf, w.zr, L, 0, w0f, goff("net2." + k + ".weight"), H, L, R,
+                              w.tpart, st);
         }
     });
 }

@@ -236,6 +236,68 @@ class SIRENAutodecoder_film(nn.Module):
                    "cfd_siren_tape_vjp")
         return gz
 
+    # -- training (K10: cfd_siren_train_grad; the loop is confild_amd.cnf_train) ----
+    def param_keys(self):
+        """Parameter keys in the library's flat-gradient order (cfd_siren_param_info)."""
+        dev = next(self.parameters()).device
+        if dev.type != "cuda":
+            raise _lib.CfdError("SIREN training needs the parameters on a GPU")
+        h, lib = self._handle(dev), _lib.load()
+        n = C.c_int()
+        _lib.check(lib.cfd_siren_num_params(h, C.byref(n)), "cfd_siren_num_params")
+        keys = []
+        for i in range(n.value):
+            k, nd, shp = C.c_char_p(), C.c_int(), (C.c_int64 * 4)()
+            _lib.check(lib.cfd_siren_param_info(h, i, C.byref(k), C.byref(nd), shp), "cfd_siren_param_info")
+            keys.append(k.value.decode())
+        return keys
+
+    def flat_params(self):
+        """(n,) fp32 device copy of every parameter, in param_keys() order."""
+        named = dict(self.named_parameters())
+        return torch.cat([named[k].detach().reshape(-1).to(torch.float32) for k in self.param_keys()]).contiguous()
+
+    def load_flat(self, flat):
+        """Copy a flat_params()-ordered buffer back into the parameters (the handle
+        re-packs its weight images on the next call)."""
+        named = dict(self.named_parameters())
+        o = 0
+        with torch.no_grad():
+            for k in self.param_keys():
+                p = named[k]
+                p.copy_(flat[o:o + p.numel()].reshape(p.shape))
+                o += p.numel()
+        if o != flat.numel():
+            raise ValueError(f"flat buffer has {flat.numel()} values, the parameters {o}")
+
+    def train_grad(self, coords, latents, rows, target, scale, grad, grad_latents, sse):
+        """One backward of MSELoss for the latent rows `rows` of the (N_samples, L)
+        table `latents` at raw coordinates (N, d) against target (R, N, c); adds
+        into grad (flat, param_keys() order), grad_latents (N_samples, L) and sse (1)."""
+        dev = latents.device
+        if dev.type != "cuda":
+            raise _lib.CfdError("SIREN training needs GPU tensors (the HIP path has no CPU fallback)")
+        d, L, c = self.in_coord_features, self.in_latent_features, self.out_features
+        cf = coords.reshape(-1, d).to(device=dev, dtype=torch.float32).contiguous()
+        N = cf.shape[0]
+        rows = rows.to(device=dev, dtype=torch.int64).contiguous()
+        R = rows.numel()
+        if torch.unique(rows).numel() != R:
+            raise ValueError("batch latent rows must be distinct")
+        tgt = target.to(device=dev, dtype=torch.float32).reshape(R, N, c).contiguous()
+        for t, name in ((latents, "latents"), (grad, "grad"), (grad_latents, "grad_latents"), (sse, "sse")):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"{name} must be a contiguous fp32 tensor on {dev}")
+        if latents.shape[-1] != L or grad_latents.shape != latents.shape:
+            raise ValueError("latents / grad_latents must be (N_samples, in_latent_features)")
+        h, lib = self._handle(dev), _lib.load()
+        n = C.c_size_t()
+        _lib.check(lib.cfd_siren_train_workspace_bytes(h, N, R, C.byref(n)), "siren train workspace")
+        ws = torch.empty(max(n.value, 16), dtype=torch.uint8, device=dev)
+        _lib.check(lib.cfd_siren_train_grad(h, _lib.ptr(cf), N, _lib.ptr(latents), _lib.ptr(rows), R, _lib.ptr(tgt),
+                                            float(scale), _lib.ptr(grad), _lib.ptr(grad_latents), _lib.ptr(sse),
+                                            _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)), "cfd_siren_train_grad")
+
     def forward(self, coords, latents):
         """nf_networks.py:480-495 (raw, un-normalised in and out)."""
         return self.decode(coords, latents)

@@ -257,6 +257,31 @@ int  cfd_siren_tape_vjp(cfd_siren* h, const float* g_out, int64_t Ns, int R,
                         const float* ymax, const float* ymin, int64_t y_stride,
                         float* g_latents, void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* CNF autodecoder training (K10; N/scripts/train.py:334-416 _single_trainer:  */
+/* model(coords, latents(idx)) -> MSELoss -> loss.backward(), Adam steps).     */
+/* ------------------------------------------------------------------------ */
+/* One backward of MSELoss(mean) for a batch: R latent rows (rows[r] indexes   *
+ * the (N_samples, L) latent table `latents`, distinct), N raw coordinates     *
+ * (N, d) as the model sees them, target (R, N, c).  scale = 2 / (numel of the *
+ * whole loss) (ATen mse_loss_backward's factor; a caller that splits the      *
+ * coordinates over several calls passes the full count).  Accumulates (+=):   *
+ *   grad          flat fp32 gradient, parameters in cfd_siren_param_info order *
+ *                 and reference shapes (torch's .grad accumulation);          *
+ *   grad_latents  (N_samples, L): the batch's rows;                           *
+ *   sse           (1) sum of squared errors of this call.                     *
+ * fp32 throughout (fp32 MFMA tape chain, fp32 MFMA weight-gradient products   *
+ * over the (row, coordinate) pairs); deterministic.                           */
+int  cfd_siren_train_workspace_bytes(const cfd_siren* h, int64_t N, int R, size_t* bytes);
+int  cfd_siren_train_grad(cfd_siren* h, const float* coords, int64_t N, const float* latents,
+                          const int64_t* rows, int R, const float* target, float scale,
+                          float* grad, float* grad_latents, float* sse,
+                          void* workspace, size_t ws_bytes, void* stream);
+/* torch.optim.Adam step (no weight decay / amsgrad) over n fp32 elements:      *
+ * exp_avg / exp_avg_sq updated in place, step = the 1-based step count.       */
+int  cfd_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   double lr, double beta1, double beta2, double eps, int64_t step, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

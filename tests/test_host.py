@@ -248,3 +248,31 @@ def test_reconstruct_frame_matches_reference():
     nanf = ReconstructFrame(g["nan_frame"][mask], mask=mask, shape=cc.POST["grid"])
     assert np.array_equal(np.isnan(nanf), np.isnan(g["nan_frame"]))
     assert np.array_equal(nanf[mask].astype(np.float32), g["nan_frame"][mask])
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_cnf_train_batch_order_is_the_dataloaders(shuffle):
+    """confild_amd.cnf_train draws the reference DataLoader's batch order
+    (train.py:375-380): the same sampler classes and the same global-RNG draws."""
+    from torch.utils.data import DataLoader, Dataset
+    from confild_amd.cnf_train import _batches
+
+    class _Idx(Dataset):
+        def __len__(self):
+            return 11
+
+        def __getitem__(self, i):
+            return i
+
+    for epoch in range(2):
+        torch.manual_seed(7 + epoch)
+        want = [b.tolist() for b in DataLoader(_Idx(), batch_size=4, shuffle=shuffle)]
+        torch.manual_seed(7 + epoch)
+        assert _batches(11, 4, shuffle, 1, 0, epoch) == want
+
+
+def test_cnf_train_distributed_batches_partition_the_samples():
+    """world_size > 1: DistributedSampler(shuffle=False) shards (train.py:361-372)."""
+    from confild_amd.cnf_train import _batches
+    got = sorted(i for r in range(2) for b in _batches(10, 3, False, 2, r, 0) for i in b)
+    assert got == list(range(10))

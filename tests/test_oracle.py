@@ -315,3 +315,36 @@ def test_oracle_case4_chain_first_step(tmp_path):
     assert np.abs(img[..., ::4, ::4].numpy() - g["img_sub"][0]).max() < 2e-5 * sc
     assert np.abs(x0[..., ::4, ::4].numpy() - g["x0_sub"][0]).max() < 2e-5
     assert abs(float(norm) - float(g["dists"][0])) < 1e-5 * float(g["dists"][0])
+
+
+def _cnftrain_case():
+    g = golden("golden_cnftrain.npz")
+    c = ast.literal_eval(str(g["case"]))
+    sd = {k: torch.from_numpy(v) for k, v in
+          synth.siren_state_dict(c["seed"], c["d"], c["L"], c["c"], c["nh"], c["H"]).items()}
+    sizes = [int(s) for s in g["batch_sizes"]]
+    order = [int(i) for i in g["batch_order"]]
+    batches, o = [], 0
+    for s in sizes:
+        batches.append(order[o:o + s])
+        o += s
+    return g, c, sd, batches
+
+
+def test_oracle_cnf_training_loop_matches_reference():
+    """oracle/cnf_train.py (the restated _single_trainer loop, train.py:385-416)
+    against the reference's own run (make_golden_train.py): first-backward
+    gradients, per-batch losses, final parameters and latents."""
+    from oracle import cnf_train as oct
+    g, c, sd, batches = _cnftrain_case()
+    sd_f, lat_f, losses, first = oct.train(sd, torch.from_numpy(g["latents0"]), torch.from_numpy(g["coords"]),
+                                           torch.from_numpy(g["fois"]), batches, c["epochs"], c["lr_nf"],
+                                           c["lr_latents"])
+    for k, v in first["net"].items():
+        ref = g["g_" + k]
+        assert np.abs(v.numpy() - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max()), k
+    assert np.abs(first["latents"].numpy() - g["g_latents"]).max() <= 1e-6 * np.abs(g["g_latents"]).max()
+    assert np.allclose(losses, g["losses"], rtol=1e-6, atol=0)
+    for k, v in sd_f.items():
+        assert np.abs(v.numpy() - g["p_" + k]).max() <= 1e-6, k
+    assert np.abs(lat_f.numpy() - g["latents_final"]).max() <= 1e-6

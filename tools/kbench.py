@@ -4,6 +4,7 @@
     python tools/kbench.py unet  [--batch 8]         # one U-Net forward
     python tools/kbench.py sweep                      # both, short
     python tools/kbench.py dps   [--batch 8]         # one DPS step (config D) and its parts
+    python tools/kbench.py train                      # one CNF training step (Case4 recipe widths)
 Prints one JSON line per measurement.
 """
 from __future__ import annotations
@@ -117,9 +118,39 @@ def bench_dps(batch=8, size=64, ns=10, dims=(3, 64, 3, 15, 384), iters=5):
     print(json.dumps(res), flush=True)
 
 
+def bench_train(rows=4, npts=65536, dims=(3, 384, 3, 15, 384), iters=3):
+    """One CNF training backward (cfd_siren_train_grad) at the Case4 recipe widths
+    (N/training_recipes/case4.yml: SIREN(3, 384, 3, 15, 384), batch 4) plus the
+    latent Adam step, on `npts` coordinates."""
+    from confild_amd.cnf_train import Adam
+    from confild_amd.nf_networks import SIRENAutodecoder_film
+    d, L, c, nh, H = dims
+    net = SIRENAutodecoder_film(d, L, c, nh, H)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, d, L, c, nh, H).items()})
+    net.to(DEV)
+    coords = torch.rand(npts, d, device=DEV) * 2 - 1
+    Z = (torch.randn(64, L, device=DEV) * 0.5).contiguous()
+    fois = torch.rand(rows, npts, c, device=DEV) * 2 - 1
+    r = torch.arange(rows, device=DEV)
+    grad = torch.zeros_like(net.flat_params())
+    gz = torch.zeros_like(Z)
+    sse = torch.zeros(1, device=DEV)
+    opt = Adam(Z, 1e-5)
+
+    def step():
+        net.train_grad(coords, Z, r, fois, 2.0 / fois.numel(), grad, gz, sse)
+        opt.step(gz)
+    med, best = timeit(step, iters=iters)
+    pairs = rows * npts
+    flops = pairs * 2 * (3 * nh * H * H + 3 * (d * H + H * c))   # forward + delta chain + weight gradients
+    print(json.dumps({"kernel": "cnf_train_step", "dims": dims, "rows": rows, "npts": npts, "ms": med,
+                      "best_ms": best, "pairs_per_s": pairs / (best / 1e3), "tflops": flops / (best / 1e3) / 1e12}),
+          flush=True)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["siren", "unet", "sweep", "dps"])
+    ap.add_argument("what", choices=["siren", "unet", "sweep", "dps", "train"])
     ap.add_argument("--latents", type=int, default=64)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=64)
@@ -135,3 +166,5 @@ if __name__ == "__main__":
         bench_unet(a.batch, a.size, bf16=a.bf16, compute=a.unet_compute, mult=a.mult)
     if a.what == "dps":
         bench_dps(a.batch, a.size)
+    if a.what == "train":
+        bench_train()
