@@ -12,6 +12,7 @@
 
 #include "sampler.hpp"
 #include "unet_kernels.hpp"
+#include "unet_train.hpp"
 
 namespace cfd {
 
@@ -314,6 +315,11 @@ struct Rec {
 struct Tape {
     Workspace* tws;
     std::vector<Rec>* recs;
+    // the timestep-embedding MLP's activations (kept for the parameter gradients):
+    // timestep_embedding (B, mc), time_embed.0 output (B, tdim), emb (B, tdim)
+    float* temb = nullptr;
+    float* th1 = nullptr;
+    float* emb = nullptr;
 };
 
 struct Sizes {
@@ -371,9 +377,14 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     const Sizes z = sizes(h);
     const bool launch = launch_req && !ws.dry && !(tape && tape->tws->dry);
     const size_t kSplitCap = split_cap(B);
-    float* temb = ws.take((size_t)B * mc);
-    float* h1 = ws.take((size_t)B * h->tdim);
-    float* emb = ws.take((size_t)B * h->tdim);
+    float* temb = tape ? tape->tws->take((size_t)B * mc) : ws.take((size_t)B * mc);
+    float* h1 = tape ? tape->tws->take((size_t)B * h->tdim) : ws.take((size_t)B * h->tdim);
+    float* emb = tape ? tape->tws->take((size_t)B * h->tdim) : ws.take((size_t)B * h->tdim);
+    if (tape) {
+        tape->temb = temb;
+        tape->th1 = h1;
+        tape->emb = emb;
+    }
     float* embo = ws.take((size_t)B * h->emb_total);
     double* gnpart = (double*)ws.take((size_t)B * cfd::kGnMaxChunks * 32 * 2 * 2);
     float* gnss = ws.take((size_t)B * 1024 * 2);
@@ -668,8 +679,18 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
 // Walks the steps in reverse; convolution input-gradients run on conv_gemm with
 // the transposed weight packs (stride-1/2 via TMODE, Upsample+conv as one 4x4
 // stride-2 convolution), GroupNorm(+SiLU) and attention backward in unet_vjp.hip.
+// Parameter gradients (K11, the TrainLoop's backward) ride on the same walk: with
+// pg != null every convolution's weight / bias gradient, every GroupNorm's gamma /
+// beta gradient, the emb_layers and time_embed gradients are accumulated (+=)
+// into pg->grad (cfd_unet_param_info order, reference shapes).
+struct ParamGrad {
+    float* grad = nullptr;
+    const float* x = nullptr;                                     // the forward's input (B, in_ch, S, S)
+    const float *temb = nullptr, *th1 = nullptr, *emb = nullptr;  // Tape's embedding activations
+};
+
 void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std::vector<Rec>& recs, Workspace& ws,
-             hipStream_t st) {
+             hipStream_t st, const ParamGrad* pg = nullptr, bool pg_ws = false) {
     const auto& c = h->cfg;
     const int S = c.image_size;
     const Sizes z = sizes(h);
@@ -683,7 +704,82 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     float* dd = ws.take((size_t)B * z.max_att);
     std::vector<float*> dhs;
     for (size_t n : z.hs) dhs.push_back(ws.take((size_t)B * n));
+    // parameter-gradient scratch (pg_ws: sized in the dry walk of cfd_unet_param_grad_workspace_bytes)
+    float *wpart = nullptr, *cpart = nullptr, *crow = nullptr, *demb = nullptr, *dth1 = nullptr, *gpp = nullptr;
+    size_t wcap = 0, ccap = 0;
+    if (pg_ws) {
+        int cmax = 0;
+        for (int l = 0; l < c.n_mult; ++l) cmax = std::max(cmax, c.channel_mult[l] * c.model_channels);
+        wcap = (size_t)16 * 3 * cmax * 2 * cmax * 9;    // <= 16 pixel slices of Cout x Ctot x 9 (qkv: 3C x C)
+        ccap = (size_t)16 * B * std::max(3 * cmax, h->tdim);
+        wpart = ws.take(wcap);
+        cpart = ws.take(ccap);    // <= 16 slices x B rows x F columns
+        crow = ws.take((size_t)B * std::max(3 * cmax, h->tdim));
+        demb = ws.take((size_t)B * h->tdim);
+        dth1 = ws.take((size_t)B * h->tdim);
+        gpp = ws.take((size_t)B * cfd::kGnMaxChunks * 2 * cmax * 2);
+    }
     if (ws.dry) return;
+    std::vector<size_t> goff;
+    {
+        size_t o = 0;
+        for (const auto& p : h->params) {
+            goff.push_back(o);
+            o += p.count;
+        }
+    }
+    auto GP = [&](const std::string& key) -> float* {
+        auto it = h->index.find(key);
+        CFD_REQUIRE(it != h->index.end(), CFD_EKEY, "internal: no parameter " + key);
+        return pg->grad + goff[it->second];
+    };
+    // weight / bias gradient of one convolution: dY (B, Hout, Wout, cout) against its forward input
+    auto wgrad = [&](const float* dy, int cout, const Act& X, const float* ss, int silu, int Hout, int Wout, int ks,
+                     int stride, int pad, int up, const std::string& pre) {
+        CFD_REQUIRE(pg_ws && cfd::wgrad_part_floats(cout, X.C(), ks, (int64_t)B * Hout * Wout) <= wcap &&
+                        cfd::colsum_part_floats((int64_t)B * Hout * Wout, cout, 1) <= ccap,
+                    CFD_ESTATE, "internal: weight-gradient scratch");
+        cfd::WgradArgs a{};
+        a.dy = dy;
+        a.src1 = X.a;
+        a.src2 = X.b;
+        a.C1 = X.Ca;
+        a.C2 = X.Cb;
+        a.Ctot = X.C();
+        a.ss = ss;
+        a.silu = silu;
+        a.part = wpart;
+        a.P = (int64_t)B * Hout * Wout;
+        a.Cout = cout;
+        a.Hin = X.H;
+        a.Win = X.W;
+        a.Hout = Hout;
+        a.Wout = Wout;
+        a.ks = ks;
+        a.stride = stride;
+        a.pad = pad;
+        a.up = up;
+        cfd::launch_conv_wgrad(a, GP(pre + ".weight"), st);
+        cfd::launch_colsum(dy, a.P, cout, 1, cpart, crow, st);
+        cfd::launch_rows_accum(crow, 1, cout, GP(pre + ".bias"), st);
+    };
+    auto gnp = [&](const Act& in, const float* ss, const float* stats, const std::string& pre, int silu,
+                   const float* dz) {
+        cfd::GnpArgs g{};
+        g.x1 = in.a;
+        g.x2 = in.b;
+        g.dz = dz;
+        g.ss = ss;
+        g.stats = stats;
+        g.part = gpp;
+        g.C1 = in.Ca;
+        g.C2 = in.Cb;
+        g.Ctot = in.C();
+        g.HW = in.H * in.W;
+        g.silu = silu;
+        cfd::launch_gn_param(g, B, GP(pre + ".weight"), GP(pre + ".bias"), st);
+    };
+    if (pg) CFD_HIP(hipMemsetAsync(demb, 0, sizeof(float) * B * h->tdim, st));
 
     auto gfree = [&](const float* b1, const float* b2 = nullptr, const float* b3 = nullptr) -> float* {
         for (auto p : gpool)
@@ -768,18 +864,24 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 cfd::launch_conv_in(a, st);
                 float* dh = gpool[1];
                 gnb(in, r.ss1, r.st1, "out.0", 1, G, nullptr, dh, nullptr);
+                if (pg) {
+                    wgrad(d_eps, c.out_channels, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, "out.2");
+                    gnp(in, r.ss1, r.st1, "out.0", 1, G);
+                }
                 dcur = Act{dh, in.Ca, nullptr, 0, in.H, in.W};
                 break;
             }
             case cfd::Step::Up: {
                 // nearest-2x + conv3x3 == one 4x4 stride-2 pad-1 convolution of dY (packed at set_param)
                 float* out = gfree(dcur.a);
+                if (pg) wgrad(dcur.a, dcur.Ca, in, nullptr, 0, dcur.H, dcur.W, 3, 1, 1, 1, s.conv);
                 dconv(dcur.a, dcur.Ca, dcur.H, dcur.W, s.conv + ".weight", s.cin, in.H, in.W, 4, 2, 1, 0, out);
                 dcur = Act{out, s.cin, nullptr, 0, in.H, in.W};
                 break;
             }
             case cfd::Step::Down: {
                 float* out = gfree(dcur.a);
+                if (pg) wgrad(dcur.a, dcur.Ca, in, nullptr, 0, dcur.H, dcur.W, 3, 2, 1, 0, s.conv);
                 dconv(dcur.a, dcur.Ca, dcur.H, dcur.W, s.conv + ".weight", s.cin, in.H, in.W, 3, 2, 1, 1, out);
                 dcur = Act{out, s.cin, nullptr, 0, in.H, in.W};
                 break;
@@ -796,19 +898,34 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 const float* dout = dcur.a;
                 float* G = gfree(dout);
                 // stride-1 3x3: plain convolutions with the mirrored packs (tpack 3)
+                const Act h1{r.h1, rs.cout, nullptr, 0, in.H, in.W};
+                if (pg) wgrad(dout, rs.cout, h1, r.ss2, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".out_layers.3");
                 dconv(dout, rs.cout, in.H, in.W, rs.pre + ".out_layers.3.weight", rs.cout, in.H, in.W, 3, 1, 1, 0, G);
+                if (pg) gnp(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G);
                 float* dh1 = gfree(dout, G);
-                gnb(Act{r.h1, rs.cout, nullptr, 0, in.H, in.W}, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr,
-                    dh1, nullptr);
+                gnb(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr, dh1, nullptr);
+                if (pg) {
+                    wgrad(dh1, rs.cout, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".in_layers.2");
+                    // emb_layers: d emb_out[b, c] = sum over pixels of dh1; its Linear(SiLU(emb))
+                    // backward, and the gradient w.r.t. emb accumulated over the ResBlocks
+                    cfd::launch_colsum(dh1, (int64_t)in.H * in.W, rs.cout, B, cpart, crow, st);
+                    const std::string ek = rs.pre + ".emb_layers.1";
+                    cfd::launch_linear_wgrad(crow, pg->emb, B, h->tdim, rs.cout, 1, GP(ek + ".weight"),
+                                             GP(ek + ".bias"), st);
+                    const float* W_emb = h->emb_w + (size_t)h->params[h->index.at(ek + ".weight")].emb_row * h->tdim;
+                    cfd::launch_linear_dgrad(crow, W_emb, pg->emb, B, h->tdim, rs.cout, 1, 1, demb, st);
+                }
                 // G <- in_layers conv input-gradient (Ctot channels)
                 dconv(dh1, rs.cout, in.H, in.W, rs.pre + ".in_layers.2.weight", in.C(), in.H, in.W, 3, 1, 1, 0, G);
                 const float* addsrc = dout;
                 if (rs.cin != rs.cout) {
+                    if (pg) wgrad(dout, rs.cout, in, nullptr, 0, in.H, in.W, 1, 1, 0, 0, rs.pre + ".skip_connection");
                     float* sk = gfree(dout, G, dh1);
                     dconv(dout, rs.cout, in.H, in.W, rs.pre + ".skip_connection.weight", in.C(), in.H, in.W, 1, 1, 0,
                           0, sk);
                     addsrc = sk;
                 }
+                if (pg) gnp(in, r.ss1, r.st1, rs.pre + ".in_layers.0", 1, G);
                 float* dx = dh1;  // dh1 is consumed: reuse for the first source's gradient
                 gnb(in, r.ss1, r.st1, rs.pre + ".in_layers.0", 1, G, addsrc, dx,
                     in.b ? dhs[r.skip_hs] : nullptr);
@@ -820,17 +937,34 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 const int T = in.H * in.W;
                 const float* dout = dcur.a;
                 float* dA = gfree(dout);
+                if (pg)
+                    wgrad(dout, at.C, Act{r.o, at.C, nullptr, 0, in.H, in.W}, nullptr, 0, in.H, in.W, 1, 1, 0, 0,
+                          at.pre + ".proj_out");
                 dconv(dout, at.C, in.H, in.W, at.pre + ".proj_out.weight", at.C, in.H, in.W, 1, 1, 0, 0, dA);
                 cfd::AttnBwdArgs ab{r.qkv, r.o, dA, r.lse, dd, dqkv, T, at.C,
                                     (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
                 cfd::launch_attention_bwd(ab, at.ch, at.heads, B, st);
+                if (pg) wgrad(dqkv, 3 * at.C, in, r.ss1, 0, in.H, in.W, 1, 1, 0, 0, at.pre + ".qkv");
                 float* dxn = gfree(dout, dA);
                 dconv(dqkv, 3 * at.C, in.H, in.W, at.pre + ".qkv.weight", at.C, in.H, in.W, 1, 1, 0, 0, dxn);
+                if (pg) gnp(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn);
                 gnb(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn, dout, dA, nullptr);
                 dcur = Act{dA, at.C, nullptr, 0, in.H, in.W};
                 break;
             }
             case cfd::Step::In: {
+                if (pg) {
+                    wgrad(dcur.a, dcur.Ca, Act{pg->x, c.in_channels, nullptr, 0, S, S}, nullptr, 0, S, S, 3, 1, 1, 0,
+                          s.conv);
+                    // time_embed: emb = L2(SiLU(L1(timestep_embedding(t)))) (unet.py:470-475,648)
+                    cfd::launch_linear_wgrad(demb, pg->th1, B, h->tdim, h->tdim, 1, GP("time_embed.2.weight"),
+                                             GP("time_embed.2.bias"), st);
+                    cfd::launch_linear_dgrad(demb, P(h, "time_embed.2.weight"), pg->th1, B, h->tdim, h->tdim, 1, 0,
+                                             dth1, st);
+                    cfd::launch_linear_wgrad(dth1, pg->temb, B, c.model_channels, h->tdim, 0,
+                                             GP("time_embed.0.weight"), GP("time_embed.0.bias"), st);
+                }
+                if (!d_x) break;
                 cfd::ConvArgs a{};
                 a.src1 = dcur.a;
                 a.C1 = dcur.Ca;
@@ -1169,6 +1303,42 @@ extern "C" int cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, i
         run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
         Workspace ws{align256(workspace), 0, false};
         run_vjp(h, d_eps, d_x, B, recs, ws, (hipStream_t)stream);
+    });
+}
+
+extern "C" int cfd_unet_param_grad_workspace_bytes(const cfd_unet* h, int B, size_t* bytes) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && bytes && B > 0, CFD_EARG, "bad argument");
+        Workspace ws{nullptr, 0, true};
+        std::vector<Rec> none;
+        run_vjp(h, nullptr, nullptr, B, none, ws, nullptr, nullptr, true);
+        *bytes = ws.off + 256;
+    });
+}
+
+extern "C" int cfd_unet_param_grad(cfd_unet* h, const float* x, const float* d_eps, int B, const void* tape,
+                                   size_t tape_bytes, float* grad, void* workspace, size_t ws_bytes, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && x && d_eps && tape && grad && workspace, CFD_EARG, "null argument");
+        CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
+        check_ready(h);
+        size_t need = 0, tneed = 0;
+        cfd_unet_param_grad_workspace_bytes(h, B, &need);
+        cfd_unet_tape_bytes(h, B, &tneed);
+        CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
+        CFD_REQUIRE(tape_bytes >= tneed, CFD_EARG, "tape too small");
+        Workspace fws{nullptr, 0, true}, tws{align256(const_cast<void*>(tape)), 0, false};
+        std::vector<Rec> recs;
+        Tape tp{&tws, &recs};
+        run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
+        ParamGrad pg;
+        pg.grad = grad;
+        pg.x = x;
+        pg.temb = tp.temb;
+        pg.th1 = tp.th1;
+        pg.emb = tp.emb;
+        Workspace ws{align256(workspace), 0, false};
+        run_vjp(h, d_eps, nullptr, B, recs, ws, (hipStream_t)stream, &pg, true);
     });
 }
 

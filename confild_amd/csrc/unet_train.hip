@@ -1,0 +1,413 @@
+// K11: parameter gradients of the latent U-Net (the diffusion TrainLoop's
+// backward, U/src/train_util.py:196-240 -> loss.backward() through
+// UNetModel.forward, U/src/unet.py:634-663), fp32, on the tape of
+// cfd_unet_forward_tape and the input-gradient walk of unet.hip:
+//   conv_wgrad_kernel   dW[co][ci][tap] = sum over output pixels p of
+//                       dY[p][co] * act(X[src(p, tap)][ci]) -- the convolution's
+//                       weight gradient as a "TN" product over pixels with the
+//                       im2col operand gathered on the fly (stride-2 / nearest-2x
+//                       addressing, two concat sources, the GroupNorm affine
+//                       (+ SiLU) of the forward's normalised input recomputed from
+//                       the raw input and its scale / shift), fp32 MFMA 16x16x4,
+//                       k (pixels) split into fixed slices added in order;
+//   colsum_kernel       per-(sample) column sums (bias and emb gradients);
+//   gn_param_kernel     GroupNorm gamma / beta gradients;
+//   linear_*_kernel     time_embed / emb_layers (B rows);
+//   ema_kernel          update_ema (U/src/nn.py:71-80).
+// Every reduction runs in a fixed order: the gradients are deterministic.
+#include <algorithm>
+
+#include "unet_kernels.hpp"
+#include "unet_train.hpp"
+
+namespace cfd {
+
+__device__ __forceinline__ float sigm_t(float x) {   // the forward SiLU's sigmoid (silu_f, unet_kernels.hip)
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896340736f));
+}
+__device__ __forceinline__ float silu_f(float x) { return x * sigm_t(x); }   // silu_f's exact arithmetic
+
+// ---------------------------------------------------------------------------
+// conv weight gradient, C[z][co][tap * Ctot + ci] over the slice z of pixels
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+    constexpr int T = 64;
+    __shared__ float Xs[16][T + 4];
+    __shared__ float Ys[16][T + 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.y * T, n0 = blockIdx.x * T;
+    const int N = a.ks * a.ks * a.Ctot, M = a.Cout;
+    const int64_t kbeg = (int64_t)blockIdx.z * a.kspan, kend = min(a.P, kbeg + a.kspan);
+    const int HWo = a.Hout * a.Wout;
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    const int kr = tid >> 4, c4 = (tid & 15) * 4;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += 16) {
+        const int64_t k = k0 + kr;
+        const bool kin = k < kend;
+        int b = 0, oy = 0, ox = 0;
+        if (kin) {
+            b = (int)(k / HWo);
+            const int rem = (int)(k - (int64_t)b * HWo);
+            oy = rem / a.Wout;
+            ox = rem - oy * a.Wout;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int m = m0 + c4 + j, n = n0 + c4 + j;
+            Xs[kr][c4 + j] = kin && m < M ? a.dy[k * M + m] : 0.f;
+            float y = 0.f;
+            if (kin && n < N) {
+                const int tap = n / a.Ctot, ci = n - tap * a.Ctot;
+                const int ty = tap / a.ks, tx = tap - ty * a.ks;
+                int iy, ix;
+                bool ok;
+                if (a.up) {   // nearest-2x input: upsampled coordinate, then halved
+                    iy = oy - a.pad + ty;
+                    ix = ox - a.pad + tx;
+                    ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                    iy >>= 1;
+                    ix >>= 1;
+                } else {
+                    iy = oy * a.stride - a.pad + ty;
+                    ix = ox * a.stride - a.pad + tx;
+                    ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+                }
+                if (ok) {
+                    const int64_t pix = ((int64_t)b * a.Hin + iy) * a.Win + ix;
+                    float v = ci < a.C1 ? a.src1[pix * a.C1 + ci] : a.src2[pix * a.C2 + (ci - a.C1)];
+                    if (a.ss) {   // the forward's GroupNorm affine (gn_apply_kernel's arithmetic) (+ SiLU)
+                        const float* s = a.ss + ((int64_t)b * a.Ctot + ci) * 2;
+                        v = v * s[0] + s[1];
+                        if (a.silu) v = silu_f(v);
+                    }
+                    y = v;
+                }
+            }
+            Ys[kr][c4 + j] = y;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 4) {
+            float fa[2], fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i] = Xs[kk + (lane >> 4)][wm * 32 + 16 * i + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) fb[j] = Ys[kk + (lane >> 4)][wn * 32 + 16 * j + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    float* Cz = a.part + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + wn * 32 + 16 * j + (lane & 15);
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * 32 + 16 * i + 4 * (lane >> 4) + r;
+                if (m < M) Cz[(int64_t)m * N + n] = acc[i][j][r];
+            }
+        }
+}
+
+// G[co][ci][tap] (the reference weight layout) += sum_z part[z][co][tap * Ctot + ci]
+__global__ __launch_bounds__(256) void wgrad_accum_kernel(const float* __restrict__ part, int Cout, int Ctot, int taps,
+                                                          int splits, float* __restrict__ G) {
+    const int64_t MN = (int64_t)Cout * Ctot * taps;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // index in G
+    if (i >= MN) return;
+    const int64_t co = i / ((int64_t)Ctot * taps);
+    const int rem = (int)(i - co * Ctot * taps), ci = rem / taps, tap = rem - ci * taps;
+    const int64_t j = co * ((int64_t)taps * Ctot) + (int64_t)tap * Ctot + ci;
+    float s = part[j];
+    for (int z = 1; z < splits; ++z) s += part[z * MN + j];
+    G[i] = G[i] + s;
+}
+
+// part[z][r][f] = sum over rows [z span, (z+1) span) of X[(r n + s) F + f] (a
+// thread per column, four rows in flight)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, float* __restrict__ part, int64_t n,
+                                                     int64_t F, int R, int64_t span) {
+    const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int r = blockIdx.y, z = blockIdx.z;
+    if (f >= F) return;
+    const int64_t s0 = z * span, s1 = min(n, s0 + span);
+    const float* src = X + ((int64_t)r * n) * F + f;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int64_t s = s0;
+    for (; s + 3 < s1; s += 4) {
+        const float v0 = src[s * F], v1 = src[(s + 1) * F], v2 = src[(s + 2) * F], v3 = src[(s + 3) * F];
+        a0 += v0;
+        a1 += v1;
+        a2 += v2;
+        a3 += v3;
+    }
+    for (; s < s1; ++s) a0 += src[s * F];
+    part[((int64_t)z * R + r) * F + f] = (a0 + a1) + (a2 + a3);
+}
+
+// out[r][f] (+)= sum_z part[z][r][f]; then, with G, G[f] += sum_r out[r][f]
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int R, int64_t F,
+                                                            int splits, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)R * F) return;
+    float s = part[i];
+    for (int z = 1; z < splits; ++z) s += part[z * R * F + i];
+    out[i] = s;
+}
+__global__ __launch_bounds__(256) void rows_accum_kernel(const float* __restrict__ rows, int R, int64_t F,
+                                                         float* __restrict__ G) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    float s = rows[f];
+    for (int r = 1; r < R; ++r) s += rows[r * F + f];
+    G[f] = G[f] + s;
+}
+
+// GroupNorm(+SiLU) parameter gradients, per (pixel chunk, sample): every thread
+// a channel quad of `rows` pixel rows; dz_eff = dy * SiLU'(z) (or dy), z = x sc +
+// sf (the forward's output before SiLU), xhat = (x - mean) rstd:
+// part[(b, chunk)][c] = (sum dz_eff xhat, sum dz_eff)
+__global__ __launch_bounds__(256) void gn_param_part_kernel(GnpArgs a) {
+    const int chunk = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    const int Ctot = a.Ctot, cq = Ctot / 4, cpg = Ctot / 32;
+    const int HW = a.HW;
+    const int p0 = (int)((int64_t)HW * chunk / a.nchunks), p1 = (int)((int64_t)HW * (chunk + 1) / a.nchunks);
+    const int rows = 256 / cq;
+    const int q = threadIdx.x % cq, r0 = threadIdx.x / cq;
+    __shared__ float red[2][1024];
+    if (r0 < rows) {
+        const int c0 = 4 * q;
+        float sc[4], sf[4], mu[4], rs[4], g1[4] = {0.f, 0.f, 0.f, 0.f}, g2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = c0 + j, grp = c / cpg;
+            sc[j] = a.ss[(b * Ctot + c) * 2];
+            sf[j] = a.ss[(b * Ctot + c) * 2 + 1];
+            mu[j] = a.stats[(b * 32 + grp) * 2];
+            rs[j] = a.stats[(b * 32 + grp) * 2 + 1];
+        }
+        for (int p = p0 + r0; p < p1; p += rows) {
+            const int64_t pix = b * HW + p;
+            const f4 x = c0 < a.C1 ? *(const f4*)(a.x1 + pix * a.C1 + c0) : *(const f4*)(a.x2 + pix * a.C2 + (c0 - a.C1));
+            const f4 dy = *(const f4*)(a.dz + pix * Ctot + c0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float d = dy[j];
+                if (a.silu) {
+                    const float z = x[j] * sc[j] + sf[j];
+                    const float s = sigm_t(z);
+                    d = d * (s * (1.0f + z * (1.0f - s)));
+                }
+                g1[j] += d * ((x[j] - mu[j]) * rs[j]);
+                g2[j] += d;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            red[0][r0 * Ctot + c0 + j] = g1[j];
+            red[1][r0 * Ctot + c0 + j] = g2[j];
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < Ctot; c += 256) {   // rows in order
+        float s1 = 0.f, s2 = 0.f;
+        for (int r = 0; r < rows; ++r) {
+            s1 += red[0][r * Ctot + c];
+            s2 += red[1][r * Ctot + c];
+        }
+        float* dst = a.part + ((b * a.nchunks + chunk) * (int64_t)Ctot + c) * 2;
+        dst[0] = s1;
+        dst[1] = s2;
+    }
+}
+
+// dgamma[c] += sum over (sample, chunk) of part, dbeta likewise, in order
+__global__ __launch_bounds__(256) void gn_param_accum_kernel(const float* __restrict__ part, int nparts, int Ctot,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= Ctot) return;
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = 0; k < nparts; ++k) {
+        s1 += part[((int64_t)k * Ctot + c) * 2];
+        s2 += part[((int64_t)k * Ctot + c) * 2 + 1];
+    }
+    dgamma[c] = dgamma[c] + s1;
+    dbeta[c] = dbeta[c] + s2;
+}
+
+// Linear(K -> N) of B rows, backward: GW[n][k] += sum_b d[b][n] f(a[b][k]),
+// Gb[n] += sum_b d[b][n]; f = SiLU when act (the layer's input is SiLU(a))
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ d, const float* __restrict__ a,
+                                                           int B, int K, int N, int act, float* __restrict__ GW,
+                                                           float* __restrict__ Gb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)N * K) return;
+    const int n = (int)(i / K), k = (int)(i - (int64_t)n * K);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) {
+        const float x = a[(int64_t)b * K + k];
+        s += d[(int64_t)b * N + n] * (act ? silu_f(x) : x);
+    }
+    GW[i] = GW[i] + s;
+    if (k == 0 && Gb) {
+        float t = 0.f;
+        for (int b = 0; b < B; ++b) t += d[(int64_t)b * N + n];
+        Gb[n] = Gb[n] + t;
+    }
+}
+
+// da[b][k] (+)= (sum_n d[b][n] W[n][k]) * (act ? SiLU'(x[b][k]) : 1)
+__global__ __launch_bounds__(256) void linear_dgrad_kernel(const float* __restrict__ d, const float* __restrict__ W,
+                                                           const float* __restrict__ x, int B, int K, int N, int act,
+                                                           int accumulate, float* __restrict__ da) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)B * K) return;
+    const int b = (int)(i / K), k = (int)(i - (int64_t)b * K);
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += d[(int64_t)b * N + n] * W[(int64_t)n * K + k];
+    if (act) {
+        const float z = x[i], sg = sigm_t(z);
+        s = s * (sg * (1.0f + z * (1.0f - sg)));
+    }
+    da[i] = accumulate ? da[i] + s : s;
+}
+
+// update_ema: targ = targ * rate + src * (1 - rate)  (targ.mul_(rate).add_(src, alpha=1 - rate))
+__global__ void ema_kernel(float* __restrict__ targ, const float* __restrict__ src, int64_t n, float rate,
+                           float omr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) targ[i] = targ[i] * rate + src[i] * omr;
+}
+
+// diffusion training loss (GaussianDiffusion.training_losses, MSE on eps,
+// gaussian_diffusion.py:775-853): x_t = sqrt(abar_t) x0 + sqrt(1 - abar_t) noise is
+// formed by the caller's q_sample; here d_eps = scale (eps - noise) with scale =
+// 2 / numel (mean_flat then the batch mean), and per-sample sums of squares
+__global__ __launch_bounds__(256) void eps_mse_kernel(const float* __restrict__ eps, const float* __restrict__ noise,
+                                                      float* __restrict__ d_eps, int64_t n_per, float scale,
+                                                      float* __restrict__ sse) {
+    const int64_t b = blockIdx.x;
+    __shared__ float red[256];
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < n_per; i += 256) {
+        const int64_t j = b * n_per + i;
+        const float d = eps[j] - noise[j];
+        d_eps[j] = d * scale;
+        s += d * d;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sse[b] = red[0];
+}
+
+// ---------------------------------------------------------------------------
+int64_t wgrad_kspan(int64_t P) {
+    const int64_t span = std::max<int64_t>(256, (P + 15) / 16);
+    return (span + 15) / 16 * 16;
+}
+
+size_t wgrad_part_floats(int Cout, int Ctot, int ks, int64_t P) {
+    const int64_t span = wgrad_kspan(P);
+    return (size_t)((P + span - 1) / span) * Cout * Ctot * ks * ks;
+}
+
+void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
+    a.kspan = wgrad_kspan(a.P);
+    const int splits = (int)((a.P + a.kspan - 1) / a.kspan);
+    const int N = a.ks * a.ks * a.Ctot;
+    const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(a.Cout, 64), (unsigned)splits);
+    hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, a);
+    check_launch("conv_wgrad_kernel");
+    const int64_t MN = (int64_t)a.Cout * N;
+    hipLaunchKernelGGL(wgrad_accum_kernel, dim3((unsigned)ceil_div(MN, 256)), dim3(256), 0, st, a.part, a.Cout,
+                       a.Ctot, a.ks * a.ks, splits, G);
+    check_launch("wgrad_accum_kernel");
+}
+
+size_t colsum_part_floats(int64_t n, int64_t F, int R) {
+    const int64_t span = wgrad_kspan(n);
+    return (size_t)((n + span - 1) / span) * R * F;
+}
+
+void launch_colsum(const float* X, int64_t n, int64_t F, int R, float* part, float* out, hipStream_t st) {
+    const int64_t span = wgrad_kspan(n);
+    const int splits = (int)((n + span - 1) / span);
+    hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)ceil_div(F, 256), R, splits), dim3(256), 0, st, X, part, n, F, R,
+                       span);
+    check_launch("colsum_kernel");
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)ceil_div((int64_t)R * F, 256)), dim3(256), 0, st, part, R,
+                       F, splits, out);
+    check_launch("colsum_reduce_kernel");
+}
+
+void launch_rows_accum(const float* rows, int R, int64_t F, float* G, hipStream_t st) {
+    hipLaunchKernelGGL(rows_accum_kernel, dim3((unsigned)ceil_div(F, 256)), dim3(256), 0, st, rows, R, F, G);
+    check_launch("rows_accum_kernel");
+}
+
+int gn_param_chunks(int HW, int Ctot) {
+    const int rows = 256 / (Ctot / 4);
+    return (int)std::min<int64_t>(kGnMaxChunks, std::max<int64_t>(1, ceil_div(HW, 16 * rows)));
+}
+
+void launch_gn_param(GnpArgs a, int B, float* dgamma, float* dbeta, hipStream_t st) {
+    a.nchunks = gn_param_chunks(a.HW, a.Ctot);
+    hipLaunchKernelGGL(gn_param_part_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
+    check_launch("gn_param_part_kernel");
+    hipLaunchKernelGGL(gn_param_accum_kernel, dim3((unsigned)ceil_div(a.Ctot, 256)), dim3(256), 0, st, a.part,
+                       a.nchunks * B, a.Ctot, dgamma, dbeta);
+    check_launch("gn_param_accum_kernel");
+}
+
+void launch_linear_wgrad(const float* d, const float* a, int B, int K, int N, int act, float* GW, float* Gb,
+                         hipStream_t st) {
+    hipLaunchKernelGGL(linear_wgrad_kernel, dim3((unsigned)ceil_div((int64_t)N * K, 256)), dim3(256), 0, st, d, a, B,
+                       K, N, act, GW, Gb);
+    check_launch("linear_wgrad_kernel");
+}
+
+void launch_linear_dgrad(const float* d, const float* W, const float* x, int B, int K, int N, int act, int accumulate,
+                         float* da, hipStream_t st) {
+    hipLaunchKernelGGL(linear_dgrad_kernel, dim3((unsigned)ceil_div((int64_t)B * K, 256)), dim3(256), 0, st, d, W, x,
+                       B, K, N, act, accumulate, da);
+    check_launch("linear_dgrad_kernel");
+}
+
+}  // namespace cfd
+
+extern "C" int cfd_ema_update(float* target, const float* source, int64_t n, double rate, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(target && source && n >= 0 && rate >= 0 && rate <= 1, CFD_EARG, "bad argument");
+        if (n == 0) return;
+        hipLaunchKernelGGL(cfd::ema_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                           target, source, n, (float)rate, (float)(1.0 - rate));
+        cfd::check_launch("ema_kernel");
+    });
+}
+
+extern "C" int cfd_eps_mse(const float* eps, const float* noise, float* d_eps, int64_t n_per_sample, int B,
+                           float scale, float* sse, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(eps && noise && d_eps && sse && n_per_sample > 0 && B > 0, CFD_EARG, "bad argument");
+        hipLaunchKernelGGL(cfd::eps_mse_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, eps, noise, d_eps,
+                           n_per_sample, scale, sse);
+        cfd::check_launch("eps_mse_kernel");
+    });
+}

@@ -1,0 +1,48 @@
+// Launch interface of the U-Net parameter-gradient kernels (unet_train.hip, K11).
+#pragma once
+#include "common.hpp"
+
+namespace cfd {
+
+// convolution weight gradient: dY (P = B Hout Wout, Cout) against the im2col of
+// the forward input (two sources; optional GroupNorm affine (+ SiLU) from ss)
+struct WgradArgs {
+    const float* dy;
+    const float* src1;
+    const float* src2;
+    const float* ss;     // (B, Ctot, 2) forward GroupNorm scale / shift, or null (raw input)
+    float* part;         // scratch: wgrad_part_floats(...)
+    int64_t P, kspan;
+    int C1, C2, Ctot, Cout;
+    int Hin, Win, Hout, Wout;
+    int ks, stride, pad, up, silu;
+};
+
+// GroupNorm(+SiLU) parameter gradient partials
+struct GnpArgs {
+    const float* x1;
+    const float* x2;
+    const float* dz;     // (B, HW, Ctot) gradient w.r.t. the GroupNorm(+SiLU) output
+    const float* ss;     // (B, Ctot, 2)
+    const float* stats;  // (B, 32, 2) mean / rstd
+    float* part;         // scratch: B * gn_param_chunks * Ctot * 2
+    int C1, C2, Ctot, HW, silu, nchunks;
+};
+
+int64_t wgrad_kspan(int64_t P);
+size_t wgrad_part_floats(int Cout, int Ctot, int ks, int64_t P);
+// G (Cout, Ctot, ks, ks) += dW
+void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st);
+size_t colsum_part_floats(int64_t n, int64_t F, int R);
+// out (R, F) = per-row-group column sums of X (R groups of n rows of F)
+void launch_colsum(const float* X, int64_t n, int64_t F, int R, float* part, float* out, hipStream_t st);
+// G (F) += sum of the R rows of rows (R, F)
+void launch_rows_accum(const float* rows, int R, int64_t F, float* G, hipStream_t st);
+int gn_param_chunks(int HW, int Ctot);
+void launch_gn_param(GnpArgs a, int B, float* dgamma, float* dbeta, hipStream_t st);
+void launch_linear_wgrad(const float* d, const float* a, int B, int K, int N, int act, float* GW, float* Gb,
+                         hipStream_t st);
+void launch_linear_dgrad(const float* d, const float* W, const float* x, int B, int K, int N, int act, int accumulate,
+                         float* da, hipStream_t st);
+
+}  // namespace cfd

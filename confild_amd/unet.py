@@ -357,6 +357,7 @@ class UNetModel(nn.Module):
                                              _lib.ptr(tape), tape.numel(), _lib.stream_of(x.device)),
                    "cfd_unet_forward_tape")
         self._taped = (x.device, B, self._signature())
+        self._tape_x = x      # the forward's input (the first convolution's weight gradient reads it)
         return eps
 
     def input_vjp(self, d_eps: torch.Tensor) -> torch.Tensor:
@@ -383,6 +384,69 @@ class UNetModel(nn.Module):
         _lib.check(lib.cfd_unet_input_vjp(h, _lib.ptr(d_eps), _lib.ptr(d_x), B, _lib.ptr(tape), tape.numel(),
                                           _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)), "cfd_unet_input_vjp")
         return d_x
+
+    def param_keys(self):
+        """Parameter keys in the library's flat-gradient order (cfd_unet_param_info)."""
+        dev = next(self.parameters()).device
+        h, lib = self._handle(dev), _lib.load()
+        n = C.c_int()
+        _lib.check(lib.cfd_unet_num_params(h, C.byref(n)), "cfd_unet_num_params")
+        keys = []
+        for i in range(n.value):
+            k, nd, shp = C.c_char_p(), C.c_int(), (C.c_int64 * 4)()
+            _lib.check(lib.cfd_unet_param_info(h, i, C.byref(k), C.byref(nd), shp), "cfd_unet_param_info")
+            keys.append(k.value.decode())
+        return keys
+
+    def flat_params(self):
+        """(n,) fp32 device copy of every parameter, in param_keys() order."""
+        named = dict(self.named_parameters())
+        return torch.cat([named[k].detach().reshape(-1).to(torch.float32) for k in self.param_keys()]).contiguous()
+
+    def load_flat(self, flat):
+        """Copy a flat_params()-ordered buffer back into the parameters (the handle
+        re-packs them on its next call)."""
+        named = dict(self.named_parameters())
+        o = 0
+        with torch.no_grad():
+            for k in self.param_keys():
+                p = named[k]
+                p.copy_(flat[o:o + p.numel()].reshape(p.shape))
+                o += p.numel()
+        if o != flat.numel():
+            raise ValueError(f"flat buffer has {flat.numel()} values, the parameters {o}")
+
+    def param_grad(self, d_eps: torch.Tensor, grad: torch.Tensor = None) -> torch.Tensor:
+        """(d eps / d params)^T d_eps for the last forward_tape, accumulated (+=) into
+        grad (flat fp32, param_keys() order; a new zero buffer when None) -- the
+        U-Net half of loss.backward() in the diffusion TrainLoop."""
+        if getattr(self, "_taped", None) is None:
+            raise RuntimeError("param_grad needs a preceding forward_tape")
+        dev, B, sig = self._taped
+        if sig != self._signature():
+            raise RuntimeError("parameters changed since forward_tape")
+        if tuple(d_eps.shape) != (B, self.out_channels, self.image_size, self.image_size) or d_eps.device != dev:
+            raise ValueError("d_eps must match the eps of the last forward_tape")
+        n_total = sum(p.numel() for p in self.parameters())
+        if grad is None:
+            grad = torch.zeros(n_total, dtype=torch.float32, device=dev)
+        if grad.numel() != n_total or grad.dtype != torch.float32 or not grad.is_contiguous() or grad.device != dev:
+            raise ValueError("grad must be a contiguous fp32 buffer of every parameter on the tape's device")
+        h = self._handle(dev)
+        lib = _lib.load()
+        d_eps = d_eps.detach().to(torch.float32).contiguous()
+        tape = self._tape_buf(h, dev, B)
+        key = ("pgrad", dev, B)
+        ws = self._pg_ws if getattr(self, "_pg_key", None) == key else None
+        if ws is None:
+            n = C.c_size_t()
+            _lib.check(lib.cfd_unet_param_grad_workspace_bytes(h, B, C.byref(n)), "param-grad workspace")
+            ws = self._pg_ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+            self._pg_key = key
+        _lib.check(lib.cfd_unet_param_grad(h, _lib.ptr(self._tape_x), _lib.ptr(d_eps), B, _lib.ptr(tape),
+                                           tape.numel(), _lib.ptr(grad), _lib.ptr(ws), ws.numel(),
+                                           _lib.stream_of(dev)), "cfd_unet_param_grad")
+        return grad
 
     def _tape_buf(self, h, device, B):
         key = (device, B)

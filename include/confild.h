@@ -277,6 +277,26 @@ int  cfd_siren_train_grad(cfd_siren* h, const float* coords, int64_t N, const fl
                           const int64_t* rows, int R, const float* target, float scale,
                           float* grad, float* grad_latents, float* sse,
                           void* workspace, size_t ws_bytes, void* stream);
+/* ------------------------------------------------------------------------ */
+/* Latent U-Net parameter gradients (K11; the diffusion TrainLoop's backward,  */
+/* U/src/train_util.py:196-240 -> loss.backward() through UNetModel.forward).  */
+/* ------------------------------------------------------------------------ */
+/* For the forward recorded by cfd_unet_forward_tape(h, x, t, ...) on `tape`:   *
+ * grad (flat fp32, cfd_unet_param_info order and reference shapes) +=         *
+ * (d eps / d params)^T d_eps -- every convolution weight / bias, GroupNorm    *
+ * gamma / beta, emb_layers and time_embed parameter; x is that forward's      *
+ * input.  fp32 (fp32 MFMA weight-gradient products over the pixels, fixed     *
+ * reduction orders: deterministic).                                           */
+int  cfd_unet_param_grad_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
+int  cfd_unet_param_grad(cfd_unet* h, const float* x, const float* d_eps, int B, const void* tape,
+                         size_t tape_bytes, float* grad, void* workspace, size_t ws_bytes, void* stream);
+/* GaussianDiffusion.training_losses' MSE term on eps (gaussian_diffusion.py    *
+ * :775-853): d_eps = scale * (eps - noise) (scale = 2 / numel for the batch    *
+ * mean of mean_flat), sse[b] = sum over sample b of (eps - noise)^2.          */
+int  cfd_eps_mse(const float* eps, const float* noise, float* d_eps, int64_t n_per_sample, int B,
+                 float scale, float* sse, void* stream);
+/* update_ema (U/src/nn.py:71-80): target = target * rate + source * (1 - rate). */
+int  cfd_ema_update(float* target, const float* source, int64_t n, double rate, void* stream);
 /* torch.optim.Adam step (no weight decay / amsgrad) over n fp32 elements:      *
  * exp_avg / exp_avg_sq updated in place, step = the 1-based step count.       */
 int  cfd_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
