@@ -108,11 +108,13 @@ _SIGS = {
     "cfd_unet_param_grad_workspace_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]),
     "cfd_unet_param_grad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t,
                                       C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
-    "cfd_eps_mse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_void_p,
-                              C.c_void_p]),
+    "cfd_eps_mse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_float,
+                              C.c_void_p, C.c_void_p]),
     "cfd_ema_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_double, C.c_void_p]),
+    "cfd_q_sample": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int,
+                               C.c_void_p]),
     "cfd_adam_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_double, C.c_double,
-                                C.c_double, C.c_double, C.c_int64, C.c_void_p]),
+                                C.c_double, C.c_double, C.c_double, C.c_int64, C.c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -27,13 +27,14 @@ from . import _lib
 
 
 class Adam:
-    """torch.optim.Adam (no weight decay, amsgrad off) over one contiguous fp32
-    device tensor, stepped by cfd_adam_step."""
+    """torch.optim.Adam (amsgrad off; weight_decay > 0: torch.optim.AdamW) over one
+    contiguous fp32 device tensor, stepped by cfd_adam_step."""
 
-    def __init__(self, param, lr, betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, param, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         if param.dtype != torch.float32 or not param.is_contiguous() or param.device.type != "cuda":
             raise ValueError("Adam needs a contiguous fp32 GPU tensor")
         self.param, self.lr, self.betas, self.eps = param, float(lr), tuple(float(b) for b in betas), float(eps)
+        self.weight_decay = float(weight_decay)   # > 0: AdamW's decoupled decay (torch.optim.AdamW)
         self.exp_avg = torch.zeros_like(param)
         self.exp_avg_sq = torch.zeros_like(param)
         self.steps = 0
@@ -45,8 +46,49 @@ class Adam:
         _lib.check(_lib.load().cfd_adam_step(_lib.ptr(self.param), _lib.ptr(grad), _lib.ptr(self.exp_avg),
                                              _lib.ptr(self.exp_avg_sq), self.param.numel(), C.c_double(self.lr),
                                              C.c_double(self.betas[0]), C.c_double(self.betas[1]),
-                                             C.c_double(self.eps), self.steps, _lib.stream_of(self.param.device)),
+                                             C.c_double(self.eps), C.c_double(self.weight_decay), self.steps,
+                                             _lib.stream_of(self.param.device)),
                    "cfd_adam_step")
+
+    def torch_state_dict(self, spans):
+        """torch.optim.Adam(W)'s state_dict for the parameters laid out in this flat
+        tensor at ``spans`` ((offset, shape) per parameter, in the optimizer's param
+        order) -- the file format of the reference's opt checkpoints."""
+        state = {}
+        if self.steps:
+            for i, (o, shp) in enumerate(spans):
+                n = 1
+                for d in shp:
+                    n *= d
+                state[i] = {"step": torch.tensor(float(self.steps)),
+                            "exp_avg": self.exp_avg[o:o + n].reshape(shp).clone(),
+                            "exp_avg_sq": self.exp_avg_sq[o:o + n].reshape(shp).clone()}
+        group = {"lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.weight_decay,
+                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                 "differentiable": False, "fused": None, "params": list(range(len(spans)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_torch_state_dict(self, sd, spans):
+        """Inverse of torch_state_dict (a reference opt checkpoint resumes here)."""
+        groups = sd["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(spans):
+            raise ValueError("optimizer state has a different parameter layout")
+        g = groups[0]
+        self.lr, self.betas, self.eps = float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"])
+        self.weight_decay = float(g.get("weight_decay", 0.0))
+        steps = set()
+        for i, (o, shp) in enumerate(spans):
+            st = sd["state"].get(i, sd["state"].get(str(i)))
+            if st is None:
+                steps.add(0)
+                continue
+            n = st["exp_avg"].numel()
+            self.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
+            self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+            steps.add(int(float(st["step"])))
+        if len(steps) != 1:
+            raise ValueError("per-parameter step counts differ; the flat optimizer keeps one")
+        self.steps = steps.pop()
 
 
 def _batches(n, batch_size, shuffle, world_size, rank, epoch, generator=None):

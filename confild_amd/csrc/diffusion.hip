@@ -351,9 +351,11 @@ extern "C" int cfd_dps_update(const float* sample, const float* g_direct, const 
 }
 
 // ---------------------------------------------------------------------------
-// Adam (torch.optim.Adam, torch/optim/adam.py _single_tensor_adam, fp32, no
-// weight decay / amsgrad): the optimiser both halves of the CNF training loop
-// step (N/scripts/train.py:385-416).  Per element, in torch's operation order:
+// Adam / AdamW (torch.optim.Adam, torch/optim/adam.py _single_tensor_adam, fp32,
+// amsgrad off; weight_decay > 0 is AdamW's decoupled decay, param *= 1 - lr wd,
+// first): the optimisers of the CNF training loop (N/scripts/train.py:385-416)
+// and of the diffusion TrainLoop (AdamW, U/src/train_util.py:78-80).  Per
+// element, in torch's operation order:
 //   exp_avg.lerp_(grad, 1 - beta1)                  (ATen lerp's two-branch form)
 //   exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
 //   denom = exp_avg_sq.sqrt() / sqrt(1 - beta2^step) + eps
@@ -363,9 +365,10 @@ extern "C" int cfd_dps_update(const float* sample, const float* g_direct, const 
 namespace cfd {
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, int64_t n, float w1, float beta2, float w2, float bc2s, float eps,
-                            float neg_step) {
+                            float neg_step, float decay) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (decay != 1.0f) p[i] = p[i] * decay;   // AdamW: param.mul_(1 - lr * weight_decay) first
     const float gi = g[i];
     float mi = m[i];
     mi = w1 < 0.5f ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
@@ -379,17 +382,18 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 }  // namespace cfd
 
 extern "C" int cfd_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
-                             double beta1, double beta2, double eps, int64_t step, void* stream) {
+                             double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream) {
     return cfd::guard([&] {
         CFD_REQUIRE(param && grad && exp_avg && exp_avg_sq && n >= 0 && step >= 1, CFD_EARG, "bad argument");
-        CFD_REQUIRE(lr >= 0 && beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1 && eps >= 0, CFD_EARG,
-                    "Adam hyper-parameters out of range");
+        CFD_REQUIRE(lr >= 0 && beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1 && eps >= 0 && weight_decay >= 0,
+                    CFD_EARG, "Adam hyper-parameters out of range");
         if (n == 0) return;
         const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
         const double step_size = lr / bc1, bc2s = std::sqrt(bc2);
         hipLaunchKernelGGL(cfd::adam_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream,
                            param, grad, exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2,
-                           (float)(1.0 - beta2), (float)bc2s, (float)eps, (float)(-step_size));
+                           (float)(1.0 - beta2), (float)bc2s, (float)eps, (float)(-step_size),
+                           (float)(1.0 - lr * weight_decay));
         cfd::check_launch("adam_kernel");
     });
 }

@@ -294,18 +294,20 @@ __global__ void ema_kernel(float* __restrict__ targ, const float* __restrict__ s
 
 // diffusion training loss (GaussianDiffusion.training_losses, MSE on eps,
 // gaussian_diffusion.py:775-853): x_t = sqrt(abar_t) x0 + sqrt(1 - abar_t) noise is
-// formed by the caller's q_sample; here d_eps = scale (eps - noise) with scale =
-// 2 / numel (mean_flat then the batch mean), and per-sample sums of squares
+// formed by the caller's q_sample; here d_eps = scale w[b] (eps - noise) with scale =
+// 2 / numel (mean_flat then the batch mean), w the schedule sampler's importance
+// weights (train_util.py:210, null = 1), and per-sample sums of squares
 __global__ __launch_bounds__(256) void eps_mse_kernel(const float* __restrict__ eps, const float* __restrict__ noise,
-                                                      float* __restrict__ d_eps, int64_t n_per, float scale,
-                                                      float* __restrict__ sse) {
+                                                      const float* __restrict__ weights, float* __restrict__ d_eps,
+                                                      int64_t n_per, float scale, float* __restrict__ sse) {
     const int64_t b = blockIdx.x;
     __shared__ float red[256];
+    const float sw = weights ? scale * weights[b] : scale;
     float s = 0.f;
     for (int64_t i = threadIdx.x; i < n_per; i += 256) {
         const int64_t j = b * n_per + i;
         const float d = eps[j] - noise[j];
-        d_eps[j] = d * scale;
+        d_eps[j] = d * sw;
         s += d * d;
     }
     red[threadIdx.x] = s;
@@ -392,6 +394,31 @@ void launch_linear_dgrad(const float* d, const float* W, const float* x, int B, 
 
 }  // namespace cfd
 
+namespace cfd {
+// q_sample (gaussian_diffusion.py:188-206): x_t = a[b] x0 + s[b] noise, a / s the
+// fp32 casts of sqrt(abar_t) / sqrt(1 - abar_t) gathered per sample
+__global__ void q_sample_kernel(const float* __restrict__ x0, const float* __restrict__ noise,
+                                const float* __restrict__ a, const float* __restrict__ s, float* __restrict__ xt,
+                                int64_t n_per, int64_t n) {
+#pragma clang fp contract(off)   // torch's two rounded products and a rounded sum: bit-exact x_t
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t b = i / n_per;
+    xt[i] = a[b] * x0[i] + s[b] * noise[i];
+}
+}  // namespace cfd
+
+extern "C" int cfd_q_sample(const float* x0, const float* noise, const float* coef_a, const float* coef_s, float* x_t,
+                            int64_t n_per_sample, int B, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(x0 && noise && coef_a && coef_s && x_t && n_per_sample > 0 && B > 0, CFD_EARG, "bad argument");
+        const int64_t n = n_per_sample * B;
+        hipLaunchKernelGGL(cfd::q_sample_kernel, dim3((unsigned)cfd::ceil_div(n, 256)), dim3(256), 0,
+                           (hipStream_t)stream, x0, noise, coef_a, coef_s, x_t, n_per_sample, n);
+        cfd::check_launch("q_sample_kernel");
+    });
+}
+
 extern "C" int cfd_ema_update(float* target, const float* source, int64_t n, double rate, void* stream) {
     return cfd::guard([&] {
         CFD_REQUIRE(target && source && n >= 0 && rate >= 0 && rate <= 1, CFD_EARG, "bad argument");
@@ -402,12 +429,12 @@ extern "C" int cfd_ema_update(float* target, const float* source, int64_t n, dou
     });
 }
 
-extern "C" int cfd_eps_mse(const float* eps, const float* noise, float* d_eps, int64_t n_per_sample, int B,
-                           float scale, float* sse, void* stream) {
+extern "C" int cfd_eps_mse(const float* eps, const float* noise, const float* weights, float* d_eps,
+                           int64_t n_per_sample, int B, float scale, float* sse, void* stream) {
     return cfd::guard([&] {
         CFD_REQUIRE(eps && noise && d_eps && sse && n_per_sample > 0 && B > 0, CFD_EARG, "bad argument");
-        hipLaunchKernelGGL(cfd::eps_mse_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, eps, noise, d_eps,
-                           n_per_sample, scale, sse);
+        hipLaunchKernelGGL(cfd::eps_mse_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, eps, noise, weights,
+                           d_eps, n_per_sample, scale, sse);
         cfd::check_launch("eps_mse_kernel");
     });
 }

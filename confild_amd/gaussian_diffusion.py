@@ -409,3 +409,84 @@ class GaussianDiffusion:
         """gaussian_diffusion.py:664-707."""
         yield from self._loop(STEP_DDIM, model, shape, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
                               device, progress, eta, step_noise, seed, sample_offset)
+
+    # -- training (the diffusion TrainLoop's loss, U/src/gaussian_diffusion.py:188-206, :744-853) ---------
+    def _train_coefs(self, t):
+        """(sqrt(abar_t), sqrt(1 - abar_t)) gathered per sample and cast to fp32, as
+        _extract_into_tensor does (:899-912): float64 table, index, .float()."""
+        dev = t.device
+        cache = self.__dict__.setdefault("_qtabs", {})
+        tabs = cache.get(dev)
+        if tabs is None:
+            tabs = (torch.from_numpy(self.sqrt_alphas_cumprod).to(dev),
+                    torch.from_numpy(self.sqrt_one_minus_alphas_cumprod).to(dev))
+            cache[dev] = tabs
+        return tabs[0][t].float().contiguous(), tabs[1][t].float().contiguous()
+
+    def q_sample(self, x_start, t, noise=None):
+        """x_t = sqrt(abar_t) x_start + sqrt(1 - abar_t) noise (:188-206), one
+        cfd_q_sample launch (bit-exact against the reference's fp32 ops)."""
+        if noise is None:
+            noise = torch.randn_like(x_start)
+        if noise.shape != x_start.shape:
+            raise ValueError("noise must have the shape of x_start")
+        if x_start.device.type != "cuda":
+            raise _lib.CfdError("q_sample runs on the GPU (cfd_q_sample)")
+        x0 = x_start.detach().to(torch.float32).contiguous()
+        nz = noise.detach().to(torch.float32).contiguous()
+        a, s = self._train_coefs(t.to(device=x0.device, dtype=torch.int64))
+        xt = torch.empty_like(x0)
+        B = x0.shape[0]
+        _lib.check(_lib.load().cfd_q_sample(_lib.ptr(x0), _lib.ptr(nz), _lib.ptr(a), _lib.ptr(s), _lib.ptr(xt),
+                                            x0.numel() // B, B, _lib.stream_of(x0.device)), "cfd_q_sample")
+        return xt
+
+    def training_losses(self, model, x_start, t, model_kwargs=None, noise=None, valid=False, weights=None,
+                        grad=None):
+        """GaussianDiffusion.training_losses (:744-853) for the MSE loss types with
+        a fixed variance: returns {"mse", "loss"} (or {"valid_mse"} when ``valid``),
+        one value per sample.
+
+        The reference's caller then runs ``(terms["loss"] * weights).mean().backward()``
+        (train_util.py:210-215); here that backward is this call's ``grad`` argument:
+        when given (the flat fp32 gradient of ``model.param_keys()``), the gradient of
+        ``(loss * weights).mean()`` (weights None = 1) is ADDED into it -- the U-Net
+        forward records its tape, cfd_eps_mse forms the loss and d eps in one pass,
+        cfd_unet_param_grad walks the network back."""
+        if model_kwargs:
+            raise NotImplementedError("class-conditional training (model_kwargs) is not on the HIP path")
+        if self.loss_type not in (LossType.MSE, LossType.RESCALED_MSE):
+            raise NotImplementedError(f"loss_type {self.loss_type} on the HIP path (the MSE losses are)")
+        if self.model_var_type not in (ModelVarType.FIXED_SMALL, ModelVarType.FIXED_LARGE):
+            raise NotImplementedError("learned variance (the vb term) is not on the HIP path")
+        if self.model_mean_type not in (ModelMeanType.EPSILON, ModelMeanType.START_X):
+            raise NotImplementedError(f"model_mean_type {self.model_mean_type} in training")
+        if valid and grad is not None:
+            raise ValueError("a validation pass has no gradient")
+        if noise is None:
+            noise = torch.randn_like(x_start)
+        x_start = x_start.detach().to(torch.float32).contiguous()
+        x_t = self.q_sample(x_start, t, noise=noise)
+        tm = self._map_timesteps(t.to(device=x_t.device))
+        with torch.no_grad():
+            out = model.forward_tape(x_t, tm) if grad is not None else model(x_t, tm)
+        target = noise if self.model_mean_type == ModelMeanType.EPSILON else x_start
+        target = target.detach().to(torch.float32).contiguous()
+        if out.shape != target.shape:
+            raise ValueError(f"model output {tuple(out.shape)} against target {tuple(target.shape)}")
+        B = out.shape[0]
+        n_per = out.numel() // B
+        sse = torch.empty(B, dtype=torch.float32, device=out.device)
+        d_out = torch.empty_like(out)
+        w = None
+        if weights is not None:
+            w = weights.detach().to(device=out.device, dtype=torch.float32).contiguous()
+        _lib.check(_lib.load().cfd_eps_mse(_lib.ptr(out), _lib.ptr(target), _lib.ptr(w),
+                                           _lib.ptr(d_out), n_per, B, C.c_float(2.0 / (B * n_per)),
+                                           _lib.ptr(sse), _lib.stream_of(out.device)), "cfd_eps_mse")
+        mse = sse / n_per
+        if valid:
+            return {"valid_mse": mse}
+        if grad is not None:
+            model.param_grad(d_out, grad)
+        return {"mse": mse, "loss": mse}

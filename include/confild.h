@@ -291,16 +291,25 @@ int  cfd_unet_param_grad_workspace_bytes(const cfd_unet* h, int B, size_t* bytes
 int  cfd_unet_param_grad(cfd_unet* h, const float* x, const float* d_eps, int B, const void* tape,
                          size_t tape_bytes, float* grad, void* workspace, size_t ws_bytes, void* stream);
 /* GaussianDiffusion.training_losses' MSE term on eps (gaussian_diffusion.py    *
- * :775-853): d_eps = scale * (eps - noise) (scale = 2 / numel for the batch    *
- * mean of mean_flat), sse[b] = sum over sample b of (eps - noise)^2.          */
-int  cfd_eps_mse(const float* eps, const float* noise, float* d_eps, int64_t n_per_sample, int B,
-                 float scale, float* sse, void* stream);
+ * :775-853) and the backward of (loss * weights).mean() (train_util.py:210):   *
+ * d_eps = scale * weights[b] * (eps - noise) (scale = 2 / numel for the batch  *
+ * mean of mean_flat; weights may be null = 1), sse[b] = sum over sample b of   *
+ * (eps - noise)^2.                                                             */
+int  cfd_eps_mse(const float* eps, const float* noise, const float* weights, float* d_eps,
+                 int64_t n_per_sample, int B, float scale, float* sse, void* stream);
 /* update_ema (U/src/nn.py:71-80): target = target * rate + source * (1 - rate). */
 int  cfd_ema_update(float* target, const float* source, int64_t n, double rate, void* stream);
-/* torch.optim.Adam step (no weight decay / amsgrad) over n fp32 elements:      *
- * exp_avg / exp_avg_sq updated in place, step = the 1-based step count.       */
+/* q_sample (U/src/gaussian_diffusion.py:188-206): x_t = coef_a[b] x0 +        *
+ * coef_s[b] noise per sample, coef_a / coef_s the fp32 casts of              *
+ * sqrt(alphas_cumprod[t]) / sqrt(1 - alphas_cumprod[t]).                      */
+int  cfd_q_sample(const float* x0, const float* noise, const float* coef_a, const float* coef_s, float* x_t,
+                  int64_t n_per_sample, int B, void* stream);
+/* torch.optim.Adam / AdamW step (amsgrad off) over n fp32 elements: exp_avg /  *
+ * exp_avg_sq updated in place, step = the 1-based step count; weight_decay > 0 *
+ * is AdamW's decoupled decay (param *= 1 - lr * weight_decay first).           */
 int  cfd_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-                   double lr, double beta1, double beta2, double eps, int64_t step, void* stream);
+                   double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                   void* stream);
 
 #ifdef __cplusplus
 }

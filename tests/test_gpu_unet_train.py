@@ -77,3 +77,99 @@ def test_unet_param_grad_accumulates_and_is_deterministic(hip):
     assert torch.equal(g1, g2)
     acc = m.param_grad(d, g1.clone())
     assert float((acc - 2 * g1).abs().max()) <= 1e-6 * float(g1.abs().max())
+
+
+class _FixedSampler:
+    """A schedule sampler replaying given timesteps (uniform weights 1)."""
+
+    def __init__(self, ts):
+        self.ts = [list(t) for t in ts]
+
+    def sample(self, batch_size, device):
+        t, self.ts[0] = self.ts[0][:batch_size], self.ts[0][batch_size:]
+        if not self.ts[0]:
+            self.ts.pop(0)
+        return torch.tensor(t, dtype=torch.int64, device=device), torch.ones(batch_size, device=device)
+
+
+def _trainloop(c, m, ts, microbatch=-1, **kw):
+    from confild_amd.script_util import create_gaussian_diffusion
+    from confild_amd.train_util import TrainLoop
+    diff = create_gaussian_diffusion(steps=1000, noise_schedule=c["schedule"], timestep_respacing="")
+    return TrainLoop(model=m, diffusion=diff, train_data=None, batch_size=c["B"], microbatch=microbatch,
+                     lr=c["lr"], ema_rate=c["ema_rate"], log_interval=1, save_interval=1000,
+                     resume_checkpoint=kw.pop("resume_checkpoint", ""), weight_decay=c["weight_decay"],
+                     schedule_sampler=_FixedSampler(ts), **kw)
+
+
+def _unpack(loop, flat):
+    named = dict(loop.model.named_parameters())
+    out, o = {}, 0
+    for k in loop.keys:
+        n = named[k].numel()
+        out[k] = flat[o:o + n].reshape(named[k].shape).cpu().numpy()
+        o += n
+    return out
+
+
+def test_trainloop_matches_reference_run(hip, tmp_path):
+    """confild_amd.train_util.TrainLoop (q_sample, eps MSE, U-Net param grads,
+    AdamW, EMA all in the library) against the reference TrainLoop's own run
+    (golden_unettrain.npz, make_golden_unet_train.py): per-step losses, the first
+    step's gradients, parameters and EMA after 2 steps (tolerances in
+    tests/unettrain_check.py); then save -> resume restores the state."""
+    from unettrain_check import check
+    g = golden("golden_unettrain.npz")
+    c = ast.literal_eval(str(g["case"]))
+    _, cfg, sd, m = _unet(c["net"])
+    loop = _trainloop(c, m, c["t"], log_dir=str(tmp_path))
+    x0 = torch.from_numpy(g["x0"]).to(DEV)
+    losses, first = [], None
+    for k in range(c["steps"]):
+        loop.run_step(x0, None, None, noise=torch.from_numpy(g["noise"][k]).to(DEV))
+        if first is None:
+            first = _unpack(loop, loop.grad)
+        losses.append(loop.logger.dumpkvs()["loss"])
+    names = [str(n) for n in g["names"]]
+    rep = check(g, c, names, losses, first, _unpack(loop, loop.params), _unpack(loop, loop.ema_params[0]),
+                rtol_loss0=2e-5, rtol_loss1=1e-4, tol_grad=2e-4, atol_grad=5e-6, tol_param=1e-4,
+                frac_loose=1e-2)
+    print(rep)
+    # the module holds the stepped parameters
+    named = dict(m.named_parameters())
+    fin = _unpack(loop, loop.params)
+    assert all(np.array_equal(named[k].detach().cpu().numpy(), fin[k]) for k in loop.keys)
+    # checkpoints in the reference's names and layouts; resume restores params / EMA / Adam state
+    loop.step = c["steps"]
+    loop.save()
+    st = c["steps"]
+    for f in (f"model{st:06d}.pt", f"ema_{c['ema_rate']}_{st:06d}.pt", f"opt{st:06d}.pt"):
+        assert (tmp_path / f).exists(), f
+    osd = torch.load(tmp_path / f"opt{st:06d}.pt", weights_only=True)
+    assert len(osd["state"]) == len(list(m.parameters())) and float(osd["state"][0]["step"]) == c["steps"]
+    _, _, _, m2 = _unet(c["net"])
+    loop2 = _trainloop(c, m2, [], resume_checkpoint=str(tmp_path / f"model{st:06d}.pt"))
+    assert loop2.resume_step == st
+    assert torch.equal(loop2.params, loop.params)
+    assert torch.equal(loop2.ema_params[0], loop.ema_params[0])
+    assert torch.equal(loop2.opt.exp_avg, loop.opt.exp_avg) and loop2.opt.steps == loop.opt.steps
+
+
+def test_trainloop_microbatches_sum_their_means(hip):
+    """forward_backward's microbatch loop (train_util.py:192-226): each
+    microbatch's (loss * weights).mean() is backpropagated and the gradients add,
+    so microbatch 1 over B = 2 gives the sum of the two one-sample gradients =
+    twice the full batch's mean gradient."""
+    g = golden("golden_unettrain.npz")
+    c = ast.literal_eval(str(g["case"]))
+    x0 = torch.from_numpy(g["x0"]).to(DEV)
+    nz = torch.from_numpy(g["noise"][0]).to(DEV)
+    grads = []
+    for mb in (-1, 1):
+        _, _, _, m = _unet(c["net"])
+        loop = _trainloop(c, m, [c["t"][0]], microbatch=mb)
+        loop.forward_backward(x0, noise=nz)
+        grads.append(loop.grad.clone())
+    full, micro = grads
+    scale = float(full.abs().max())
+    assert float((micro - 2 * full).abs().max()) <= 2e-5 * scale

@@ -276,3 +276,46 @@ def test_cnf_train_distributed_batches_partition_the_samples():
     from confild_amd.cnf_train import _batches
     got = sorted(i for r in range(2) for b in _batches(10, 3, False, 2, r, 0) for i in b)
     assert got == list(range(10))
+
+
+def test_schedule_samplers_match_reference_draws():
+    """confild_amd.resample (U/src/resample.py): UniformSampler draws with the
+    reference's numpy call (np.random.choice over p = w / sum(w), weights
+    1 / (T p[t]) -- exactly 1 for the uniform case); LossSecondMomentResampler
+    stays uniform until every step has history_per_term losses, then weights by
+    the RMS of the recent losses mixed with uniform_prob."""
+    from confild_amd.resample import LossSecondMomentResampler, create_named_schedule_sampler
+    diff = create_gaussian_diffusion(steps=50, noise_schedule="cosine")
+    s = create_named_schedule_sampler("uniform", diff)
+    np.random.seed(3)
+    t, w = s.sample(7, "cpu")
+    np.random.seed(3)
+    assert t.tolist() == np.random.choice(50, size=(7,), p=np.ones(50) / 50).tolist()
+    assert t.dtype == torch.int64 and torch.equal(w, torch.ones(7))
+    ls = LossSecondMomentResampler(diff, history_per_term=2, uniform_prob=0.1)
+    ts = list(range(50))
+    ls.update_with_all_losses(ts, [1.0] * 50)
+    assert np.array_equal(ls.weights(), np.ones(50))
+    ls.update_with_local_losses(torch.arange(50), torch.arange(50, dtype=torch.float32))
+    w = ls.weights()
+    rms = np.sqrt((1.0 + np.arange(50.0) ** 2) / 2)
+    assert np.allclose(w, rms / rms.sum() * 0.9 + 0.1 / 50)
+    with pytest.raises(NotImplementedError):
+        create_named_schedule_sampler("nope", diff)
+
+
+def test_trainloop_host_side():
+    """TrainLoop helpers (train_util.py:298-331) and its loud refusals."""
+    from confild_amd.train_util import TrainLoop, find_ema_checkpoint, parse_resume_step_from_filename
+    assert parse_resume_step_from_filename("/a/b/model012345.pt") == 12345
+    assert parse_resume_step_from_filename("/a/b/ema.pt") == 0
+    assert find_ema_checkpoint(None, 3, 0.9) is None
+    m = create_model(image_size=16, num_channels=32, num_res_blocks=1, attention_resolutions="8",
+                     channel_mult="1,2")
+    diff = create_gaussian_diffusion(steps=100, noise_schedule="cosine")
+    kw = dict(model=m, diffusion=diff, train_data=None, batch_size=2, microbatch=-1, lr=1e-4, ema_rate="0.9999",
+              log_interval=1, save_interval=1, resume_checkpoint="")
+    with pytest.raises(NotImplementedError):
+        TrainLoop(**kw, use_fp16=True)
+    with pytest.raises(_lib.CfdError):
+        TrainLoop(**kw)                      # a CPU model: the loop runs on the GPU only

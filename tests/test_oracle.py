@@ -348,3 +348,28 @@ def test_oracle_cnf_training_loop_matches_reference():
     for k, v in sd_f.items():
         assert np.abs(v.numpy() - g["p_" + k]).max() <= 1e-6, k
     assert np.abs(lat_f.numpy() - g["latents_final"]).max() <= 1e-6
+
+
+def test_oracle_unet_trainloop_matches_reference():
+    """oracle/unet_train.py (the restated TrainLoop step: q_sample, eps MSE,
+    backward, AdamW, EMA; train_util.py:178-226) against the reference's own run
+    (make_golden_unet_train.py): losses, first-step gradients, parameters and
+    EMA after two steps (tolerances: tests/unettrain_check.py)."""
+    from oracle import unet_train as out
+    from unettrain_check import check
+    g = golden("golden_unettrain.npz")
+    c = ast.literal_eval(str(g["case"]))
+    kw = ast.literal_eval(str(g["kwargs"]))
+    cfg = ou.Config(**kw)
+    shapes = ou.param_shapes(cfg)
+    sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(int(g["weight_seed"]), shapes).items()}
+    names = [str(n) for n in g["names"]]
+    assert sorted(names) == sorted(sd)
+    sd_f, ema, losses, first = out.train(sd, cfg, torch.from_numpy(g["x0"]), c["t"],
+                                         [torch.from_numpy(n) for n in g["noise"]], c["lr"], c["weight_decay"],
+                                         c["ema_rate"], c["schedule"])
+    rep = check(g, c, names, losses, {k: v.numpy() for k, v in first.items()},
+                {k: v.numpy() for k, v in sd_f.items()}, {k: v.numpy() for k, v in ema.items()},
+                rtol_loss0=1e-6, rtol_loss1=1e-5, tol_grad=1e-5, atol_grad=1e-7, tol_param=1e-6,
+                frac_loose=1e-3)
+    print(rep)
