@@ -79,6 +79,12 @@ struct cfd_unet {
     mutable std::map<int, size_t> ws_cache;  // workspace bytes per B (the dry walk is host work)
     uint64_t version = 0;   // bumped by every set_param / set_compute: launch arguments (weight
                             // scales, kernel choice) captured into a graph are stale after it
+    // device repack (cfd_unet_load_flat): descriptor table, block -> parameter map, amax scratch
+    void* rp_desc = nullptr;
+    int64_t* rp_first = nullptr;   // (nparams + 1) first block of each parameter
+    float* rp_part = nullptr;      // (nblocks, 2) per-block |max| (forward pack, input-gradient pack)
+    float* rp_amax = nullptr;      // (nparams, 2)
+    int64_t rp_blocks = 0;
 };
 
 namespace {
@@ -706,14 +712,16 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     for (size_t n : z.hs) dhs.push_back(ws.take((size_t)B * n));
     // parameter-gradient scratch (pg_ws: sized in the dry walk of cfd_unet_param_grad_workspace_bytes)
     float *wpart = nullptr, *cpart = nullptr, *crow = nullptr, *demb = nullptr, *dth1 = nullptr, *gpp = nullptr;
+    float* wact = nullptr;
     size_t wcap = 0, ccap = 0;
     if (pg_ws) {
         int cmax = 0;
         for (int l = 0; l < c.n_mult; ++l) cmax = std::max(cmax, c.channel_mult[l] * c.model_channels);
         wcap = (size_t)16 * 3 * cmax * 2 * cmax * 9;    // <= 16 pixel slices of Cout x Ctot x 9 (qkv: 3C x C)
-        ccap = (size_t)16 * B * std::max(3 * cmax, h->tdim);
+        ccap = (size_t)(256 + B) * std::max(3 * cmax, h->tdim);
         wpart = ws.take(wcap);
-        cpart = ws.take(ccap);    // <= 16 slices x B rows x F columns
+        cpart = ws.take(ccap);    // colsum_part_floats: <= 256 + B (slice, row) pairs of F columns
+        wact = ws.take((size_t)B * z.max_cat);   // the activated input of a weight-gradient product
         crow = ws.take((size_t)B * std::max(3 * cmax, h->tdim));
         demb = ws.take((size_t)B * h->tdim);
         dth1 = ws.take((size_t)B * h->tdim);
@@ -736,10 +744,12 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     // weight / bias gradient of one convolution: dY (B, Hout, Wout, cout) against its forward input
     auto wgrad = [&](const float* dy, int cout, const Act& X, const float* ss, int silu, int Hout, int Wout, int ks,
                      int stride, int pad, int up, const std::string& pre) {
-        CFD_REQUIRE(pg_ws && cfd::wgrad_part_floats(cout, X.C(), ks, (int64_t)B * Hout * Wout) <= wcap &&
-                        cfd::colsum_part_floats((int64_t)B * Hout * Wout, cout, 1) <= ccap,
+        CFD_REQUIRE(pg_ws && cfd::colsum_part_floats((int64_t)B * Hout * Wout, cout, 1) <= ccap &&
+                        (size_t)cout * X.C() * ks * ks <= wcap && (size_t)X.H * X.W * X.C() <= z.max_cat,
                     CFD_ESTATE, "internal: weight-gradient scratch");
         cfd::WgradArgs a{};
+        a.part_cap = (int64_t)wcap;
+        a.act = wact;
         a.dy = dy;
         a.src1 = X.a;
         a.src2 = X.b;
@@ -1045,6 +1055,10 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->arena_thi);
     (void)hipFree(h->arena_tlo);
     (void)hipFree(h->nonfinite);
+    (void)hipFree(h->rp_desc);
+    (void)hipFree(h->rp_first);
+    (void)hipFree(h->rp_part);
+    (void)hipFree(h->rp_amax);
     delete h;
 }
 
@@ -1166,6 +1180,249 @@ extern "C" int cfd_unet_set_param(cfd_unet* h, const char* key, const float* hos
             CFD_HIP(hipMemcpy(h->arena_tlo + p.toffset, tlo.data(), pk.size() * 2, hipMemcpyHostToDevice));
         }
         p.set = true;
+        ++h->version;
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Device repack of every parameter (cfd_unet_load_flat): the packing of
+// cfd_unet_set_param above, element for element, in three launches -- per-block
+// |max| of each pack, per-parameter reduction, then the pack writes.  Each
+// parameter spans ceil(max(count, tcount) / RP_CHUNK) blocks (tcount: the
+// input-gradient pack's element count, 16 Cin Cout for the upsample pack).
+namespace cfd {
+constexpr int RP_CHUNK = 4096;
+
+struct RepackDesc {
+    int64_t src, count, off, toff, tcount;
+    int pack, tpack, co, ci, taps, emb_row;
+};
+
+__device__ __forceinline__ int rp_param(const int64_t* __restrict__ first, int np, int64_t blk) {
+    int lo = 0, hi = np;   // largest p with first[p] <= blk
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (first[mid] <= blk) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// the upsample pack's value at its element e (the 4x4 stride-2 kernel of
+// nearest-2x + conv3x3: per axis e0 = w2, e1 = w1 + w2, e2 = w0 + w1, e3 = w0),
+// summed in cfd_unet_set_param's order
+__device__ __forceinline__ float rp_up_value(const float* __restrict__ w, const RepackDesc& d, int64_t e) {
+    const int64_t o = e % d.co, r = e / d.co;
+    const int q = (int)(r % 16);
+    const int64_t i = r / 16;
+    const int ey = q >> 2, ex = q & 3;
+    const int dlo_y = ey == 0 ? 2 : ey == 1 ? 1 : 0, dhi_y = ey == 0 ? 2 : ey == 1 ? 2 : ey == 2 ? 1 : 0;
+    const int dlo_x = ex == 0 ? 2 : ex == 1 ? 1 : 0, dhi_x = ex == 0 ? 2 : ex == 1 ? 2 : ex == 2 ? 1 : 0;
+    const float* base = w + (o * d.ci + i) * 9;
+    float v = 0.f;
+    for (int dy = dlo_y; dy <= dhi_y; ++dy)
+        for (int dx = dlo_x; dx <= dhi_x; ++dx) v += base[dy * 3 + dx];
+    return v;
+}
+
+__global__ __launch_bounds__(256) void rp_amax_kernel(const float* __restrict__ flat,
+                                                      const RepackDesc* __restrict__ desc,
+                                                      const int64_t* __restrict__ first, int np,
+                                                      float* __restrict__ part) {
+    const int64_t blk = blockIdx.x;
+    const int p = rp_param(first, np, blk);
+    const RepackDesc d = desc[p];
+    const float* w = flat + d.src;
+    const int64_t e0 = (blk - first[p]) * RP_CHUNK;
+    float m0 = 0.f, m1 = 0.f;
+    for (int64_t e = e0 + threadIdx.x; e < e0 + RP_CHUNK; e += 256) {
+        if (e < d.count) m0 = fmaxf(m0, fabsf(w[e]));
+        if (d.tpack == 2 && e < d.tcount) m1 = fmaxf(m1, fabsf(rp_up_value(w, d, e)));
+    }
+    __shared__ float r0[256], r1[256];
+    r0[threadIdx.x] = m0;
+    r1[threadIdx.x] = m1;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            r0[threadIdx.x] = fmaxf(r0[threadIdx.x], r0[threadIdx.x + s]);
+            r1[threadIdx.x] = fmaxf(r1[threadIdx.x], r1[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[blk * 2] = r0[0];
+        part[blk * 2 + 1] = d.tpack == 2 ? r1[0] : r0[0];   // the other packs permute the weights
+    }
+}
+
+__global__ __launch_bounds__(256) void rp_reduce_kernel(const float* __restrict__ part,
+                                                        const int64_t* __restrict__ first, float* __restrict__ amax) {
+    const int p = blockIdx.x;
+    float m0 = 0.f, m1 = 0.f;
+    for (int64_t b = first[p] + threadIdx.x; b < first[p + 1]; b += 256) {
+        m0 = fmaxf(m0, part[b * 2]);
+        m1 = fmaxf(m1, part[b * 2 + 1]);
+    }
+    __shared__ float r0[256], r1[256];
+    r0[threadIdx.x] = m0;
+    r1[threadIdx.x] = m1;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            r0[threadIdx.x] = fmaxf(r0[threadIdx.x], r0[threadIdx.x + s]);
+            r1[threadIdx.x] = fmaxf(r1[threadIdx.x], r1[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        amax[p * 2] = r0[0];
+        amax[p * 2 + 1] = r1[0];
+    }
+}
+
+__device__ __forceinline__ uint16_t rp_bf16(float f) {   // to_bf16 (host) bit for bit
+    const uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ float rp_scale(float amax) {   // 2^-e, e the frexp exponent of amax (1 for 0)
+    if (!(amax > 0.f)) return 1.f;
+    int ex;
+    frexpf(amax, &ex);
+    return ldexpf(1.f, -ex);
+}
+
+__device__ __forceinline__ void rp_split(float v, float s, _Float16* hi, _Float16* lo, int64_t i) {
+#pragma clang fp contract(off)
+    const float x = v * s;
+    const _Float16 h = (_Float16)x;
+    hi[i] = h;
+    lo[i] = (_Float16)(x - (float)h);
+}
+
+__global__ __launch_bounds__(256) void rp_pack_kernel(const float* __restrict__ flat,
+                                                      const RepackDesc* __restrict__ desc,
+                                                      const int64_t* __restrict__ first, int np,
+                                                      const float* __restrict__ amax, float* __restrict__ arena,
+                                                      uint16_t* __restrict__ arena_bf, _Float16* __restrict__ arena_hi,
+                                                      _Float16* __restrict__ arena_lo, float* __restrict__ arena_t,
+                                                      _Float16* __restrict__ arena_thi,
+                                                      _Float16* __restrict__ arena_tlo, float* __restrict__ emb_w,
+                                                      float* __restrict__ emb_b, int tdim) {
+    const int64_t blk = blockIdx.x;
+    const int p = rp_param(first, np, blk);
+    const RepackDesc d = desc[p];
+    const float* w = flat + d.src;
+    const int64_t e0 = (blk - first[p]) * RP_CHUNK;
+    const float s = rp_scale(amax[p * 2]), ts = rp_scale(amax[p * 2 + 1]);
+    const bool conv = d.pack == (int)Pack::Conv1 || d.pack == (int)Pack::Conv3;
+    for (int64_t e = e0 + threadIdx.x; e < e0 + RP_CHUNK; e += 256) {
+        if (e < d.count) {
+            const float v = w[e];
+            if (d.pack == (int)Pack::Raw) {
+                arena[d.off + e] = v;
+            } else if (d.pack == (int)Pack::EmbW) {
+                emb_w[(int64_t)d.emb_row * tdim + e] = v;
+            } else if (d.pack == (int)Pack::EmbB) {
+                emb_b[d.emb_row + e] = v;
+            } else {
+                int64_t j = e;
+                if (d.pack == (int)Pack::Conv3) {   // (o, i, tap) -> (o, tap, i)
+                    const int64_t tap = e % 9, oi = e / 9, i = oi % d.ci, o = oi / d.ci;
+                    j = (o * 9 + tap) * d.ci + i;
+                }
+                arena[d.off + j] = v;
+                arena_bf[d.off + j] = rp_bf16(v);
+                rp_split(v, s, arena_hi, arena_lo, d.off + j);
+            }
+            if (conv && (d.tpack == 1 || d.tpack == 3)) {   // (o, i, tap) -> (i, tap', o)
+                const int64_t tap = e % d.taps, oi = e / d.taps, i = oi % d.ci, o = oi / d.ci;
+                const int64_t tt = d.tpack == 3 ? d.taps - 1 - tap : tap;
+                const int64_t j = (i * d.taps + tt) * d.co + o;
+                arena_t[d.toff + j] = v;
+                rp_split(v, ts, arena_thi, arena_tlo, d.toff + j);
+            }
+        }
+        if (d.tpack == 2 && e < d.tcount) {
+            const float v = rp_up_value(w, d, e);
+            arena_t[d.toff + e] = v;
+            rp_split(v, ts, arena_thi, arena_tlo, d.toff + e);
+        }
+    }
+}
+}  // namespace cfd
+
+extern "C" int cfd_unet_load_flat(cfd_unet* h, const float* flat, size_t n, void* stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h && flat, CFD_EARG, "null argument");
+        const int np = (int)h->params.size();
+        size_t total = 0;
+        for (const auto& p : h->params) total += p.count;
+        CFD_REQUIRE(n == total, CFD_ESHAPE, "flat buffer size differs from the parameter count");
+        cfd::DeviceGuard dg(h->device);
+        hipStream_t st = (hipStream_t)stream;
+        if (!h->rp_desc) {
+            std::vector<cfd::RepackDesc> desc(np);
+            std::vector<int64_t> first(np + 1);
+            int64_t src = 0, blocks = 0;
+            for (int k = 0; k < np; ++k) {
+                const auto& p = h->params[k];
+                cfd::RepackDesc d{};
+                d.src = src;
+                d.count = (int64_t)p.count;
+                d.off = (int64_t)p.offset;
+                d.toff = (int64_t)p.toffset;
+                d.pack = (int)p.pack;
+                d.tpack = p.tpack;
+                d.emb_row = p.emb_row;
+                d.co = p.shape.size() > 1 ? (int)p.shape[0] : 1;
+                d.ci = p.shape.size() > 1 ? (int)p.shape[1] : 1;
+                d.taps = (int)(d.count / std::max<int64_t>(1, (int64_t)d.co * d.ci));
+                d.tcount = p.tpack == 2 ? (int64_t)d.ci * 16 * d.co : d.count;
+                if (p.tpack == 2) CFD_REQUIRE(d.taps == 9, CFD_ESTATE, "internal: upsample pack needs 3x3");
+                desc[k] = d;
+                first[k] = blocks;
+                blocks += std::max<int64_t>(1, cfd::ceil_div(std::max(d.count, d.tcount), cfd::RP_CHUNK));
+                src += d.count;
+            }
+            first[np] = blocks;
+            CFD_HIP(hipMalloc(&h->rp_desc, sizeof(cfd::RepackDesc) * np));
+            CFD_HIP(hipMalloc(&h->rp_first, sizeof(int64_t) * (np + 1)));
+            CFD_HIP(hipMalloc(&h->rp_part, sizeof(float) * 2 * blocks));
+            CFD_HIP(hipMalloc(&h->rp_amax, sizeof(float) * 2 * np));
+            CFD_HIP(hipMemcpy(h->rp_desc, desc.data(), sizeof(cfd::RepackDesc) * np, hipMemcpyHostToDevice));
+            CFD_HIP(hipMemcpy(h->rp_first, first.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice));
+            h->rp_blocks = blocks;
+        }
+        const auto* desc = (const cfd::RepackDesc*)h->rp_desc;
+        hipLaunchKernelGGL(cfd::rp_amax_kernel, dim3((unsigned)h->rp_blocks), dim3(256), 0, st, flat, desc,
+                           h->rp_first, np, h->rp_part);
+        cfd::check_launch("rp_amax_kernel");
+        hipLaunchKernelGGL(cfd::rp_reduce_kernel, dim3(np), dim3(256), 0, st, h->rp_part, h->rp_first, h->rp_amax);
+        cfd::check_launch("rp_reduce_kernel");
+        hipLaunchKernelGGL(cfd::rp_pack_kernel, dim3((unsigned)h->rp_blocks), dim3(256), 0, st, flat, desc,
+                           h->rp_first, np, h->rp_amax, h->arena, h->arena_bf, (_Float16*)h->arena_hi,
+                           (_Float16*)h->arena_lo, h->arena_t, (_Float16*)h->arena_thi, (_Float16*)h->arena_tlo,
+                           h->emb_w, h->emb_b, h->tdim);
+        cfd::check_launch("rp_pack_kernel");
+        std::vector<float> amax(2 * (size_t)np);
+        CFD_HIP(hipMemcpyAsync(amax.data(), h->rp_amax, sizeof(float) * 2 * np, hipMemcpyDeviceToHost, st));
+        CFD_HIP(hipStreamSynchronize(st));
+        for (int k = 0; k < np; ++k) {
+            auto& p = h->params[k];
+            if (p.pack == Pack::Conv1 || p.pack == Pack::Conv3) {
+                int ex = 0;
+                if (amax[2 * k] > 0.f) std::frexp(amax[2 * k], &ex);
+                p.split_inv = std::ldexp(1.0f, ex);
+            }
+            if (p.tpack) {
+                int ex = 0;
+                if (amax[2 * k + 1] > 0.f) std::frexp(amax[2 * k + 1], &ex);
+                p.tsplit_inv = std::ldexp(1.0f, ex);
+            }
+            p.set = true;
+        }
         ++h->version;
     });
 }

@@ -121,6 +121,125 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
         }
 }
 
+// The same product on 128 x 128 tiles when the tile's 128 columns lie in one tap
+// (Ctot % 128 == 0, every level of the recipe U-Nets): the pixel decode is per
+// row, the input quads are float4 loads of one source (the activated copy `act`
+// when the forward applied GroupNorm (+ SiLU), else the raw sources), the next
+// 16-pixel slice is prefetched into registers while the MFMAs run on this one.
+__global__ __launch_bounds__(256) void conv_wgrad128_kernel(WgradArgs a, const float* __restrict__ act) {
+    constexpr int T = 128, KS = 16;
+    __shared__ __attribute__((aligned(16))) float Xs[KS][T + 4];
+    __shared__ __attribute__((aligned(16))) float Ys[KS][T + 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.y * T, n0 = blockIdx.x * T;
+    const int M = a.Cout, N = a.ks * a.ks * a.Ctot;
+    const int tap = n0 / a.Ctot, ci0 = n0 - tap * a.Ctot;
+    const int ty = tap / a.ks, tx = tap - ty * a.ks;
+    const int64_t kbeg = (int64_t)blockIdx.z * a.kspan, kend = min(a.P, kbeg + a.kspan);
+    const int HWo = a.Hout * a.Wout;
+    const int cq = (tid & 31) * 4, rq = tid >> 5;   // column quad; rows rq and rq + 8
+    f4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    f4 xv[2], yv[2];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int64_t k = k0 + rq + 8 * hh;
+            f4 x = f4{0.f, 0.f, 0.f, 0.f}, y = f4{0.f, 0.f, 0.f, 0.f};
+            if (k < kend) {
+                if (m0 + cq < M) x = *(const f4*)(a.dy + k * M + m0 + cq);
+                const int b = (int)(k / HWo);
+                const int rem = (int)(k - (int64_t)b * HWo);
+                const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+                int iy, ix;
+                bool ok;
+                if (a.up) {
+                    iy = oy - a.pad + ty;
+                    ix = ox - a.pad + tx;
+                    ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                    iy >>= 1;
+                    ix >>= 1;
+                } else {
+                    iy = oy * a.stride - a.pad + ty;
+                    ix = ox * a.stride - a.pad + tx;
+                    ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+                }
+                if (ok) {
+                    const int64_t pix = ((int64_t)b * a.Hin + iy) * a.Win + ix;
+                    const int ci = ci0 + cq;
+                    if (act)
+                        y = *(const f4*)(act + pix * a.Ctot + ci);
+                    else
+                        y = ci < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + ci)
+                                      : *(const f4*)(a.src2 + pix * a.C2 + (ci - a.C1));
+                }
+            }
+            xv[hh] = x;
+            yv[hh] = y;
+        }
+    };
+    load(kbeg);
+    for (int64_t k0 = kbeg; k0 < kend; k0 += KS) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            *(f4*)&Xs[rq + 8 * hh][cq] = xv[hh];
+            *(f4*)&Ys[rq + 8 * hh][cq] = yv[hh];
+        }
+        __syncthreads();
+        if (k0 + KS < kend) load(k0 + KS);
+#pragma unroll
+        for (int kk = 0; kk < KS; kk += 4) {
+            float fa[4], fb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fa[i] = Xs[kk + (lane >> 4)][wm * 64 + 16 * i + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) fb[j] = Ys[kk + (lane >> 4)][wn * 64 + 16 * j + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    float* Cz = a.part + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + 16 * j + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+                if (m < M) Cz[(int64_t)m * N + n] = acc[i][j][r];
+            }
+        }
+}
+
+// act (B, Hin, Win, Ctot) = the forward's GroupNorm affine (+ SiLU) of the two
+// sources, once per layer for conv_wgrad128_kernel (conv_wgrad_kernel's arithmetic)
+__global__ __launch_bounds__(256) void gn_act_kernel(WgradArgs a, int64_t nquads) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nquads) return;
+    const int cqn = a.Ctot / 4;
+    const int64_t pix = i / cqn;
+    const int c = (int)(i - pix * cqn) * 4;
+    const int64_t b = pix / ((int64_t)a.Hin * a.Win);
+    f4 v = c < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c) : *(const f4*)(a.src2 + pix * a.C2 + (c - a.C1));
+    const float* s = a.ss + (b * a.Ctot + c) * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float x = v[j] * s[2 * j] + s[2 * j + 1];
+        if (a.silu) x = silu_f(x);
+        v[j] = x;
+    }
+    *(f4*)(a.act + pix * a.Ctot + c) = v;
+}
+
 // G[co][ci][tap] (the reference weight layout) += sum_z part[z][co][tap * Ctot + ci]
 __global__ __launch_bounds__(256) void wgrad_accum_kernel(const float* __restrict__ part, int Cout, int Ctot, int taps,
                                                           int splits, float* __restrict__ G) {
@@ -135,36 +254,71 @@ __global__ __launch_bounds__(256) void wgrad_accum_kernel(const float* __restric
     G[i] = G[i] + s;
 }
 
-// part[z][r][f] = sum over rows [z span, (z+1) span) of X[(r n + s) F + f] (a
-// thread per column, four rows in flight)
+// part[z][r][f] = sum over rows [z span, (z+1) span) of X[(r n + s) F + f]: a
+// block per (slice, row group), threads over (row lane, column group of VW), the
+// row lanes combined in order through LDS
+template <int VW>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, float* __restrict__ part, int64_t n,
                                                      int64_t F, int R, int64_t span) {
-    const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int r = blockIdx.y, z = blockIdx.z;
-    if (f >= F) return;
-    const int64_t s0 = z * span, s1 = min(n, s0 + span);
-    const float* src = X + ((int64_t)r * n) * F + f;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int64_t s = s0;
-    for (; s + 3 < s1; s += 4) {
-        const float v0 = src[s * F], v1 = src[(s + 1) * F], v2 = src[(s + 2) * F], v3 = src[(s + 3) * F];
-        a0 += v0;
-        a1 += v1;
-        a2 += v2;
-        a3 += v3;
+    typedef float vt __attribute__((ext_vector_type(VW)));
+    const int z = blockIdx.x, r = blockIdx.y;
+    const int G = (int)(F / VW);
+    const int64_t s0 = (int64_t)z * span, s1 = min(n, s0 + span);
+    const float* src = X + (int64_t)r * n * F;
+    float* dst = part + ((int64_t)z * R + r) * F;
+    if (G >= 256) {   // one row lane: every thread walks whole columns
+        for (int cg = threadIdx.x; cg < G; cg += 256) {
+            vt a0 = (vt)0.f, a1 = (vt)0.f;
+            int64_t s = s0;
+            for (; s + 1 < s1; s += 2) {
+                a0 += *(const vt*)(src + s * F + cg * VW);
+                a1 += *(const vt*)(src + (s + 1) * F + cg * VW);
+            }
+            if (s < s1) a0 += *(const vt*)(src + s * F + cg * VW);
+            *(vt*)(dst + cg * VW) = a0 + a1;
+        }
+        return;
     }
-    for (; s < s1; ++s) a0 += src[s * F];
-    part[((int64_t)z * R + r) * F + f] = (a0 + a1) + (a2 + a3);
+    const int L = 256 / G, rl = threadIdx.x / G, cg = threadIdx.x - rl * G;
+    __shared__ float red[256 * VW];
+    vt a0 = (vt)0.f, a1 = (vt)0.f;
+    if (rl < L) {
+        int64_t s = s0 + rl;
+        for (; s + L < s1; s += 2 * L) {
+            a0 += *(const vt*)(src + s * F + cg * VW);
+            a1 += *(const vt*)(src + (s + L) * F + cg * VW);
+        }
+        if (s < s1) a0 += *(const vt*)(src + s * F + cg * VW);
+        *(vt*)(red + (rl * G + cg) * VW) = a0 + a1;
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < G * VW; f += 256) {
+        float t = 0.f;
+        for (int l = 0; l < L; ++l) t += red[l * G * VW + f];
+        dst[f] = t;
+    }
 }
 
-// out[r][f] (+)= sum_z part[z][r][f]; then, with G, G[f] += sum_r out[r][f]
+// out[r][f] = sum_z part[z][r][f] (a block per 64 columns of a row, 4 slice lanes
+// combined in order)
 __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int R, int64_t F,
                                                             int splits, float* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)R * F) return;
-    float s = part[i];
-    for (int z = 1; z < splits; ++z) s += part[z * R * F + i];
-    out[i] = s;
+    const int r = blockIdx.y, zl = threadIdx.x >> 6;
+    const int64_t f = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    __shared__ float red[4][64];
+    float a0 = 0.f, a1 = 0.f;
+    if (f < F) {
+        int z = zl;
+        for (; z + 4 < splits; z += 8) {
+            a0 += part[((int64_t)z * R + r) * F + f];
+            a1 += part[((int64_t)(z + 4) * R + r) * F + f];
+        }
+        if (z < splits) a0 += part[((int64_t)z * R + r) * F + f];
+    }
+    red[zl][threadIdx.x & 63] = a0 + a1;
+    __syncthreads();
+    if (threadIdx.x < 64 && f < F)
+        out[(int64_t)r * F + f] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 __global__ __launch_bounds__(256) void rows_accum_kernel(const float* __restrict__ rows, int R, int64_t F,
                                                          float* __restrict__ G) {
@@ -234,18 +388,30 @@ __global__ __launch_bounds__(256) void gn_param_part_kernel(GnpArgs a) {
     }
 }
 
-// dgamma[c] += sum over (sample, chunk) of part, dbeta likewise, in order
+// dgamma[c] += sum over (sample, chunk) of part, dbeta likewise: a block per 32
+// channels, 8 part lanes combined in order
 __global__ __launch_bounds__(256) void gn_param_accum_kernel(const float* __restrict__ part, int nparts, int Ctot,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= Ctot) return;
+    const int pl = threadIdx.x >> 5, c = blockIdx.x * 32 + (threadIdx.x & 31);
+    __shared__ float red[8][32][2];
     float s1 = 0.f, s2 = 0.f;
-    for (int k = 0; k < nparts; ++k) {
-        s1 += part[((int64_t)k * Ctot + c) * 2];
-        s2 += part[((int64_t)k * Ctot + c) * 2 + 1];
+    if (c < Ctot)
+        for (int k = pl; k < nparts; k += 8) {
+            s1 += part[((int64_t)k * Ctot + c) * 2];
+            s2 += part[((int64_t)k * Ctot + c) * 2 + 1];
+        }
+    red[pl][threadIdx.x & 31][0] = s1;
+    red[pl][threadIdx.x & 31][1] = s2;
+    __syncthreads();
+    if (threadIdx.x < 32 && c < Ctot) {
+        float t1 = 0.f, t2 = 0.f;
+        for (int l = 0; l < 8; ++l) {
+            t1 += red[l][threadIdx.x][0];
+            t2 += red[l][threadIdx.x][1];
+        }
+        dgamma[c] = dgamma[c] + t1;
+        dbeta[c] = dbeta[c] + t2;
     }
-    dgamma[c] = dgamma[c] + s1;
-    dbeta[c] = dbeta[c] + s2;
 }
 
 // Linear(K -> N) of B rows, backward: GW[n][k] += sum_b d[b][n] f(a[b][k]),
@@ -320,42 +486,81 @@ __global__ __launch_bounds__(256) void eps_mse_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-int64_t wgrad_kspan(int64_t P) {
-    const int64_t span = std::max<int64_t>(256, (P + 15) / 16);
+namespace {
+bool wgrad_fast(const WgradArgs& a) {
+    return a.Ctot % 128 == 0 && a.Cout % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0;
+}
+}  // namespace
+
+// pixel slices: the 64-tile kernel >= 256 pixels a slice, at most 16 slices; the
+// 128-tile kernel enough slices for ~2048 blocks (<= 64, >= 256 pixels a slice,
+// partials within part_cap)
+int64_t wgrad_kspan(const WgradArgs& a) {
+    int64_t splits;
+    if (wgrad_fast(a)) {
+        const int64_t N = (int64_t)a.ks * a.ks * a.Ctot, MN = (int64_t)a.Cout * N;
+        const int64_t tiles = ceil_div(N, 128) * ceil_div(a.Cout, 128);
+        splits = std::min<int64_t>({64, ceil_div(2048, tiles), ceil_div(a.P, 256), std::max<int64_t>(1, a.part_cap / MN)});
+        splits = std::max<int64_t>(1, splits);
+        const int64_t span = ceil_div(a.P, splits);
+        return (span + 15) / 16 * 16;
+    }
+    const int64_t span = std::max<int64_t>(256, (a.P + 15) / 16);
     return (span + 15) / 16 * 16;
 }
 
-size_t wgrad_part_floats(int Cout, int Ctot, int ks, int64_t P) {
-    const int64_t span = wgrad_kspan(P);
-    return (size_t)((P + span - 1) / span) * Cout * Ctot * ks * ks;
+size_t wgrad_part_floats(const WgradArgs& a) {
+    const int64_t span = wgrad_kspan(a);
+    return (size_t)((a.P + span - 1) / span) * a.Cout * a.Ctot * a.ks * a.ks;
 }
 
 void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
-    a.kspan = wgrad_kspan(a.P);
+    a.kspan = wgrad_kspan(a);
     const int splits = (int)((a.P + a.kspan - 1) / a.kspan);
     const int N = a.ks * a.ks * a.Ctot;
-    const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(a.Cout, 64), (unsigned)splits);
-    hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, a);
-    check_launch("conv_wgrad_kernel");
+    CFD_REQUIRE(wgrad_part_floats(a) <= (size_t)a.part_cap, CFD_ESTATE, "internal: weight-gradient scratch");
+    if (wgrad_fast(a)) {
+        const float* act = nullptr;
+        if (a.ss) {
+            CFD_REQUIRE(a.act, CFD_ESTATE, "internal: activation scratch");
+            const int64_t nq = (int64_t)(a.P / ((int64_t)a.Hout * a.Wout)) * a.Hin * a.Win * (a.Ctot / 4);
+            hipLaunchKernelGGL(gn_act_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a, nq);
+            check_launch("gn_act_kernel");
+            act = a.act;
+        }
+        const dim3 grid((unsigned)(N / 128), (unsigned)ceil_div(a.Cout, 128), (unsigned)splits);
+        hipLaunchKernelGGL(conv_wgrad128_kernel, grid, dim3(256), 0, st, a, act);
+        check_launch("conv_wgrad128_kernel");
+    } else {
+        const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(a.Cout, 64), (unsigned)splits);
+        hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, a);
+        check_launch("conv_wgrad_kernel");
+    }
     const int64_t MN = (int64_t)a.Cout * N;
     hipLaunchKernelGGL(wgrad_accum_kernel, dim3((unsigned)ceil_div(MN, 256)), dim3(256), 0, st, a.part, a.Cout,
                        a.Ctot, a.ks * a.ks, splits, G);
     check_launch("wgrad_accum_kernel");
 }
 
-size_t colsum_part_floats(int64_t n, int64_t F, int R) {
-    const int64_t span = wgrad_kspan(n);
-    return (size_t)((n + span - 1) / span) * R * F;
+namespace {
+int colsum_splits(int64_t n, int R) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(256, R), ceil_div(n, 64)));
 }
+}  // namespace
+
+size_t colsum_part_floats(int64_t n, int64_t F, int R) { return (size_t)colsum_splits(n, R) * R * F; }
 
 void launch_colsum(const float* X, int64_t n, int64_t F, int R, float* part, float* out, hipStream_t st) {
-    const int64_t span = wgrad_kspan(n);
-    const int splits = (int)((n + span - 1) / span);
-    hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)ceil_div(F, 256), R, splits), dim3(256), 0, st, X, part, n, F, R,
-                       span);
+    const int splits = colsum_splits(n, R);
+    const int64_t span = ceil_div(n, splits);
+    const bool v4 = F % 4 == 0 && ((uintptr_t)X & 15) == 0;
+    if (v4)
+        hipLaunchKernelGGL(colsum_kernel<4>, dim3(splits, R), dim3(256), 0, st, X, part, n, F, R, span);
+    else
+        hipLaunchKernelGGL(colsum_kernel<1>, dim3(splits, R), dim3(256), 0, st, X, part, n, F, R, span);
     check_launch("colsum_kernel");
-    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)ceil_div((int64_t)R * F, 256)), dim3(256), 0, st, part, R,
-                       F, splits, out);
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)ceil_div(F, 64), R), dim3(256), 0, st, part, R, F,
+                       splits, out);
     check_launch("colsum_reduce_kernel");
 }
 
@@ -364,16 +569,17 @@ void launch_rows_accum(const float* rows, int R, int64_t F, float* G, hipStream_
     check_launch("rows_accum_kernel");
 }
 
-int gn_param_chunks(int HW, int Ctot) {
-    const int rows = 256 / (Ctot / 4);
-    return (int)std::min<int64_t>(kGnMaxChunks, std::max<int64_t>(1, ceil_div(HW, 16 * rows)));
+int gn_param_chunks(int HW, int Ctot, int B) {   // ~256 blocks over the batch, >= 16 row passes a chunk
+    const int rows = std::max(1, 256 / (Ctot / 4));
+    const int64_t want = std::max<int64_t>(1, ceil_div(256, B));
+    return (int)std::min<int64_t>({kGnMaxChunks, want, std::max<int64_t>(1, ceil_div(HW, 16 * rows))});
 }
 
 void launch_gn_param(GnpArgs a, int B, float* dgamma, float* dbeta, hipStream_t st) {
-    a.nchunks = gn_param_chunks(a.HW, a.Ctot);
+    a.nchunks = gn_param_chunks(a.HW, a.Ctot, B);
     hipLaunchKernelGGL(gn_param_part_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
     check_launch("gn_param_part_kernel");
-    hipLaunchKernelGGL(gn_param_accum_kernel, dim3((unsigned)ceil_div(a.Ctot, 256)), dim3(256), 0, st, a.part,
+    hipLaunchKernelGGL(gn_param_accum_kernel, dim3((unsigned)ceil_div(a.Ctot, 32)), dim3(256), 0, st, a.part,
                        a.nchunks * B, a.Ctot, dgamma, dbeta);
     check_launch("gn_param_accum_kernel");
 }

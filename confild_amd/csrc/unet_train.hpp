@@ -11,8 +11,9 @@ struct WgradArgs {
     const float* src1;
     const float* src2;
     const float* ss;     // (B, Ctot, 2) forward GroupNorm scale / shift, or null (raw input)
-    float* part;         // scratch: wgrad_part_floats(...)
-    int64_t P, kspan;
+    float* part;         // scratch: wgrad_part_floats(a) floats (<= part_cap)
+    float* act;          // scratch (B, Hin, Win, Ctot) for the activated input of the 128-tile path, or null
+    int64_t P, kspan, part_cap;
     int C1, C2, Ctot, Cout;
     int Hin, Win, Hout, Wout;
     int ks, stride, pad, up, silu;
@@ -29,8 +30,9 @@ struct GnpArgs {
     int C1, C2, Ctot, HW, silu, nchunks;
 };
 
-int64_t wgrad_kspan(int64_t P);
-size_t wgrad_part_floats(int Cout, int Ctot, int ks, int64_t P);
+// pixel slice of one block (P, Cout, Ctot, ks and part_cap of a set)
+int64_t wgrad_kspan(const WgradArgs& a);
+size_t wgrad_part_floats(const WgradArgs& a);
 // G (Cout, Ctot, ks, ks) += dW
 void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st);
 size_t colsum_part_floats(int64_t n, int64_t F, int R);
@@ -38,7 +40,7 @@ size_t colsum_part_floats(int64_t n, int64_t F, int R);
 void launch_colsum(const float* X, int64_t n, int64_t F, int R, float* part, float* out, hipStream_t st);
 // G (F) += sum of the R rows of rows (R, F)
 void launch_rows_accum(const float* rows, int R, int64_t F, float* G, hipStream_t st);
-int gn_param_chunks(int HW, int Ctot);
+int gn_param_chunks(int HW, int Ctot, int B);
 void launch_gn_param(GnpArgs a, int B, float* dgamma, float* dbeta, hipStream_t st);
 void launch_linear_wgrad(const float* d, const float* a, int B, int K, int N, int act, float* GW, float* Gb,
                          hipStream_t st);

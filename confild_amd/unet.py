@@ -387,6 +387,8 @@ class UNetModel(nn.Module):
 
     def param_keys(self):
         """Parameter keys in the library's flat-gradient order (cfd_unet_param_info)."""
+        if getattr(self, "_pkeys", None) is not None:
+            return list(self._pkeys)
         dev = next(self.parameters()).device
         h, lib = self._handle(dev), _lib.load()
         n = C.c_int()
@@ -396,6 +398,7 @@ class UNetModel(nn.Module):
             k, nd, shp = C.c_char_p(), C.c_int(), (C.c_int64 * 4)()
             _lib.check(lib.cfd_unet_param_info(h, i, C.byref(k), C.byref(nd), shp), "cfd_unet_param_info")
             keys.append(k.value.decode())
+        self._pkeys = tuple(keys)      # the topology is fixed at construction
         return keys
 
     def flat_params(self):
@@ -404,17 +407,27 @@ class UNetModel(nn.Module):
         return torch.cat([named[k].detach().reshape(-1).to(torch.float32) for k in self.param_keys()]).contiguous()
 
     def load_flat(self, flat):
-        """Copy a flat_params()-ordered buffer back into the parameters (the handle
-        re-packs them on its next call)."""
+        """Copy a flat_params()-ordered buffer back into the parameters.  On the
+        handle's device the library re-packs from it on the GPU (cfd_unet_load_flat:
+        one repack of every kernel layout, no host round trip); elsewhere the handle
+        re-packs on its next call."""
         named = dict(self.named_parameters())
+        keys = self.param_keys()
+        n = sum(named[k].numel() for k in keys)
+        if flat.numel() != n:
+            raise ValueError(f"flat buffer has {flat.numel()} values, the parameters {n}")
         o = 0
         with torch.no_grad():
-            for k in self.param_keys():
+            for k in keys:
                 p = named[k]
                 p.copy_(flat[o:o + p.numel()].reshape(p.shape))
                 o += p.numel()
-        if o != flat.numel():
-            raise ValueError(f"flat buffer has {flat.numel()} values, the parameters {o}")
+        dev = flat.device
+        entry = self._handles.get(dev.index) if dev.type == "cuda" else None
+        if entry is not None and entry[1] is not None and flat.dtype == torch.float32 and flat.is_contiguous():
+            _lib.check(_lib.load().cfd_unet_load_flat(entry[0], _lib.ptr(flat), n, _lib.stream_of(dev)),
+                       "cfd_unet_load_flat")
+            entry[1] = self._signature()
 
     def param_grad(self, d_eps: torch.Tensor, grad: torch.Tensor = None) -> torch.Tensor:
         """(d eps / d params)^T d_eps for the last forward_tape, accumulated (+=) into

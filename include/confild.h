@@ -70,6 +70,14 @@ int  cfd_unet_set_param(cfd_unet* h, const char* key, const float* host_data, si
 int  cfd_unet_set_time_freqs(cfd_unet* h, const float* host_freqs, int n);
 /* Fails with CFD_ESTATE until every parameter has been set. */
 int  cfd_unet_ready(const cfd_unet* h);
+/* Every parameter at once from a DEVICE buffer: `flat` holds the fp32 tensors
+ * in cfd_unet_param_info order, reference layout, n floats in total.  Packs on
+ * the device (the same layouts, bf16 copy, split-f16 hi / lo with the same
+ * power-of-two scales as cfd_unet_set_param, bit for bit) on `stream` and
+ * synchronises it once (the split scales are launch arguments).  The training
+ * loop's parameter update (train_util.py: the optimizer writes the weights the
+ * next forward reads).                                                         */
+int  cfd_unet_load_flat(cfd_unet* h, const float* flat, size_t n, void* stream);
 int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
 /* eps = UNetModel.forward(x, timesteps): x (B,1,H,W), t (B) int64 (already
  * remapped through timestep_map, respace.py:123-128), eps (B,1,H,W). */

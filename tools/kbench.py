@@ -5,6 +5,7 @@
     python tools/kbench.py sweep                      # both, short
     python tools/kbench.py dps   [--batch 8]         # one DPS step (config D) and its parts
     python tools/kbench.py train                      # one CNF training step (Case4 recipe widths)
+    python tools/kbench.py utrain --batch 16 --size 128   # one diffusion TrainLoop step (Case1 recipe)
 Prints one JSON line per measurement.
 """
 from __future__ import annotations
@@ -148,9 +149,43 @@ def bench_train(rows=4, npts=65536, dims=(3, 384, 3, 15, 384), iters=3):
           flush=True)
 
 
+def bench_unet_train(batch=16, size=128, mult="", iters=5):
+    """One diffusion TrainLoop.run_step (U/src/train_util.py:178-226: q_sample,
+    U-Net forward with tape, eps MSE, parameter gradients, AdamW, EMA) at the
+    recipe widths (U/training_recipes/case1.yml: 128^2, batch 16, 128 channels,
+    lr 5e-5, EMA 0.9999), and its parts."""
+    from confild_amd.script_util import create_gaussian_diffusion, create_model
+    from confild_amd.train_util import TrainLoop
+    m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
+                     attention_resolutions="32,16,8", channel_mult=mult)
+    sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.to(DEV)
+    diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine")
+    loop = TrainLoop(model=m, diffusion=diff, train_data=None, batch_size=batch, microbatch=-1, lr=5e-5,
+                     ema_rate="0.9999", log_interval=1000, save_interval=10000, resume_checkpoint="")
+    x0 = torch.rand(batch, 1, size, size, device=DEV) * 2 - 1
+    res = {"kernel": "unet_train_step", "batch": batch, "size": size, "mult": mult,
+           "n_params": loop.params.numel()}
+    res["step_ms"], best = timeit(lambda: loop.run_step(x0), iters=iters, warm=2)
+    res["samples_per_s"] = batch / (best / 1e3)
+    t = torch.randint(0, 1000, (batch,), device=DEV)
+    x = torch.randn_like(x0)
+    res["fwd_tape_ms"], _ = timeit(lambda: m.forward_tape(x, t), iters=iters)
+    d = torch.randn_like(x0)
+    res["param_grad_ms"], _ = timeit(lambda: m.param_grad(d, loop.grad), iters=iters)
+    res["adamw_ms"], _ = timeit(lambda: loop.opt.step(loop.grad), iters=iters)
+    res["ema_ms"], _ = timeit(loop._update_ema, iters=iters)
+    res["load_flat_ms"], _ = timeit(lambda: m.load_flat(loop.params), iters=iters)
+    gf = {64: 68.61, 128: 140.75}.get(size)
+    if gf and not mult:
+        res["tflops_3x_fwd"] = 3 * batch * gf * 1e9 / (best / 1e3) / 1e12
+    print(json.dumps(res), flush=True)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["siren", "unet", "sweep", "dps", "train"])
+    ap.add_argument("what", choices=["siren", "unet", "sweep", "dps", "train", "utrain"])
     ap.add_argument("--latents", type=int, default=64)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=64)
@@ -168,3 +203,5 @@ if __name__ == "__main__":
         bench_dps(a.batch, a.size)
     if a.what == "train":
         bench_train()
+    if a.what == "utrain":
+        bench_unet_train(a.batch, a.size, a.mult)
