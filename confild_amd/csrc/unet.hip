@@ -1317,35 +1317,36 @@ __global__ __launch_bounds__(256) void rp_pack_kernel(const float* __restrict__ 
     const int64_t e0 = (blk - first[p]) * RP_CHUNK;
     const float s = rp_scale(amax[p * 2]), ts = rp_scale(amax[p * 2 + 1]);
     const bool conv = d.pack == (int)Pack::Conv1 || d.pack == (int)Pack::Conv3;
+    // e walks the DESTINATION layouts (coalesced writes; the reads gather)
     for (int64_t e = e0 + threadIdx.x; e < e0 + RP_CHUNK; e += 256) {
         if (e < d.count) {
-            const float v = w[e];
             if (d.pack == (int)Pack::Raw) {
-                arena[d.off + e] = v;
+                arena[d.off + e] = w[e];
             } else if (d.pack == (int)Pack::EmbW) {
-                emb_w[(int64_t)d.emb_row * tdim + e] = v;
+                emb_w[(int64_t)d.emb_row * tdim + e] = w[e];
             } else if (d.pack == (int)Pack::EmbB) {
-                emb_b[d.emb_row + e] = v;
+                emb_b[d.emb_row + e] = w[e];
             } else {
-                int64_t j = e;
-                if (d.pack == (int)Pack::Conv3) {   // (o, i, tap) -> (o, tap, i)
-                    const int64_t tap = e % 9, oi = e / 9, i = oi % d.ci, o = oi / d.ci;
-                    j = (o * 9 + tap) * d.ci + i;
+                int64_t src = e;
+                if (d.pack == (int)Pack::Conv3) {   // dst (o, tap, i) <- src (o, i, tap)
+                    const int64_t i = e % d.ci, ot = e / d.ci, tap = ot % 9, o = ot / 9;
+                    src = (o * d.ci + i) * 9 + tap;
                 }
-                arena[d.off + j] = v;
-                arena_bf[d.off + j] = rp_bf16(v);
-                rp_split(v, s, arena_hi, arena_lo, d.off + j);
-            }
-            if (conv && (d.tpack == 1 || d.tpack == 3)) {   // (o, i, tap) -> (i, tap', o)
-                const int64_t tap = e % d.taps, oi = e / d.taps, i = oi % d.ci, o = oi / d.ci;
-                const int64_t tt = d.tpack == 3 ? d.taps - 1 - tap : tap;
-                const int64_t j = (i * d.taps + tt) * d.co + o;
-                arena_t[d.toff + j] = v;
-                rp_split(v, ts, arena_thi, arena_tlo, d.toff + j);
+                const float v = w[src];
+                arena[d.off + e] = v;
+                arena_bf[d.off + e] = rp_bf16(v);
+                rp_split(v, s, arena_hi, arena_lo, d.off + e);
             }
         }
-        if (d.tpack == 2 && e < d.tcount) {
-            const float v = rp_up_value(w, d, e);
+        if (conv && d.tpack && e < d.tcount) {
+            float v;
+            if (d.tpack == 2) {
+                v = rp_up_value(w, d, e);
+            } else {   // dst (i, tap', o) <- src (o, i, tap), tap' = tap (1) or taps - 1 - tap (3)
+                const int64_t o = e % d.co, r = e / d.co, tt = r % d.taps, i = r / d.taps;
+                const int64_t tap = d.tpack == 3 ? d.taps - 1 - tt : tt;
+                v = w[(o * d.ci + i) * d.taps + tap];
+            }
             arena_t[d.toff + e] = v;
             rp_split(v, ts, arena_thi, arena_tlo, d.toff + e);
         }

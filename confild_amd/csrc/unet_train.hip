@@ -123,11 +123,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 
 // The same product on 128 x 128 tiles when the tile's 128 columns lie in one tap
 // (Ctot % 128 == 0, every level of the recipe U-Nets): the pixel decode is per
-// row, the input quads are float4 loads of one source (the activated copy `act`
-// when the forward applied GroupNorm (+ SiLU), else the raw sources), the next
-// 16-pixel slice is prefetched into registers while the MFMAs run on this one.
+// row (32-bit), the input quads are float4 loads of one source (the activated copy
+// `act` when the forward applied GroupNorm (+ SiLU), else the raw sources), the
+// next 32-pixel slice is prefetched into registers while the MFMAs run on this one.
 __global__ __launch_bounds__(256) void conv_wgrad128_kernel(WgradArgs a, const float* __restrict__ act) {
-    constexpr int T = 128, KS = 16;
+    constexpr int T = 128, KS = 32, RW = KS / 8;   // rows a thread stages: rq + 8 r
     __shared__ __attribute__((aligned(16))) float Xs[KS][T + 4];
     __shared__ __attribute__((aligned(16))) float Ys[KS][T + 4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -136,24 +136,24 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(WgradArgs a, const f
     const int M = a.Cout, N = a.ks * a.ks * a.Ctot;
     const int tap = n0 / a.Ctot, ci0 = n0 - tap * a.Ctot;
     const int ty = tap / a.ks, tx = tap - ty * a.ks;
-    const int64_t kbeg = (int64_t)blockIdx.z * a.kspan, kend = min(a.P, kbeg + a.kspan);
+    const int kbeg = (int)(blockIdx.z * a.kspan), kend = (int)min(a.P, (int64_t)kbeg + a.kspan);   // P < 2^31
     const int HWo = a.Hout * a.Wout;
-    const int cq = (tid & 31) * 4, rq = tid >> 5;   // column quad; rows rq and rq + 8
+    const int cq = (tid & 31) * 4, rq = tid >> 5;   // column quad; rows rq + 8 r
     f4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    f4 xv[2], yv[2];
-    auto load = [&](int64_t k0) {
+    f4 xv[RW], yv[RW];
+    auto load = [&](int k0) {
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int64_t k = k0 + rq + 8 * hh;
+        for (int hh = 0; hh < RW; ++hh) {
+            const int k = k0 + rq + 8 * hh;
             f4 x = f4{0.f, 0.f, 0.f, 0.f}, y = f4{0.f, 0.f, 0.f, 0.f};
             if (k < kend) {
-                if (m0 + cq < M) x = *(const f4*)(a.dy + k * M + m0 + cq);
-                const int b = (int)(k / HWo);
-                const int rem = (int)(k - (int64_t)b * HWo);
+                if (m0 + cq < M) x = *(const f4*)(a.dy + (int64_t)k * M + m0 + cq);
+                const int b = k / HWo;
+                const int rem = k - b * HWo;
                 const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
                 int iy, ix;
                 bool ok;
@@ -183,9 +183,9 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(WgradArgs a, const f
         }
     };
     load(kbeg);
-    for (int64_t k0 = kbeg; k0 < kend; k0 += KS) {
+    for (int k0 = kbeg; k0 < kend; k0 += KS) {
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
+        for (int hh = 0; hh < RW; ++hh) {
             *(f4*)&Xs[rq + 8 * hh][cq] = xv[hh];
             *(f4*)&Ys[rq + 8 * hh][cq] = yv[hh];
         }
@@ -435,20 +435,35 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
     }
 }
 
-// da[b][k] (+)= (sum_n d[b][n] W[n][k]) * (act ? SiLU'(x[b][k]) : 1)
+// da[b][k] (+)= (sum_n d[b][n] W[n][k]) * (act ? SiLU'(x[b][k]) : 1): a block per
+// (sample, 32 columns k), 8 lanes over n (coalesced rows of W) combined in order
 __global__ __launch_bounds__(256) void linear_dgrad_kernel(const float* __restrict__ d, const float* __restrict__ W,
                                                            const float* __restrict__ x, int B, int K, int N, int act,
                                                            int accumulate, float* __restrict__ da) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)B * K) return;
-    const int b = (int)(i / K), k = (int)(i - (int64_t)b * K);
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s += d[(int64_t)b * N + n] * W[(int64_t)n * K + k];
-    if (act) {
-        const float z = x[i], sg = sigm_t(z);
-        s = s * (sg * (1.0f + z * (1.0f - sg)));
+    const int b = blockIdx.y, nl = threadIdx.x >> 5, k = blockIdx.x * 32 + (threadIdx.x & 31);
+    __shared__ float red[8][32];
+    float s0 = 0.f, s1 = 0.f;
+    if (k < K) {
+        const float* dr = d + (int64_t)b * N;
+        int n = nl;
+        for (; n + 8 < N; n += 16) {
+            s0 += dr[n] * W[(int64_t)n * K + k];
+            s1 += dr[n + 8] * W[(int64_t)(n + 8) * K + k];
+        }
+        if (n < N) s0 += dr[n] * W[(int64_t)n * K + k];
     }
-    da[i] = accumulate ? da[i] + s : s;
+    red[nl][threadIdx.x & 31] = s0 + s1;
+    __syncthreads();
+    if (threadIdx.x < 32 && k < K) {
+        float s = 0.f;
+        for (int l = 0; l < 8; ++l) s += red[l][threadIdx.x];
+        const int64_t i = (int64_t)b * K + k;
+        if (act) {
+            const float z = x[i], sg = sigm_t(z);
+            s = s * (sg * (1.0f + z * (1.0f - sg)));
+        }
+        da[i] = accumulate ? da[i] + s : s;
+    }
 }
 
 // update_ema: targ = targ * rate + src * (1 - rate)  (targ.mul_(rate).add_(src, alpha=1 - rate))
@@ -503,9 +518,15 @@ int64_t wgrad_kspan(const WgradArgs& a) {
         splits = std::min<int64_t>({64, ceil_div(2048, tiles), ceil_div(a.P, 256), std::max<int64_t>(1, a.part_cap / MN)});
         splits = std::max<int64_t>(1, splits);
         const int64_t span = ceil_div(a.P, splits);
-        return (span + 15) / 16 * 16;
+        return (span + 31) / 32 * 32;
     }
-    const int64_t span = std::max<int64_t>(256, (a.P + 15) / 16);
+    // 64-tile kernel (thin layers: the 1-channel input / output convolutions, narrow
+    // test topologies): ~1024 blocks, <= 128 slices of >= 256 pixels
+    const int64_t N = (int64_t)a.ks * a.ks * a.Ctot, MN = (int64_t)a.Cout * N;
+    const int64_t tiles = ceil_div(N, 64) * ceil_div(a.Cout, 64);
+    splits = std::min<int64_t>({128, ceil_div(1024, tiles), ceil_div(a.P, 256), std::max<int64_t>(1, a.part_cap / MN)});
+    splits = std::max<int64_t>(1, splits);
+    const int64_t span = ceil_div(a.P, splits);
     return (span + 15) / 16 * 16;
 }
 
@@ -520,6 +541,7 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
     const int N = a.ks * a.ks * a.Ctot;
     CFD_REQUIRE(wgrad_part_floats(a) <= (size_t)a.part_cap, CFD_ESTATE, "internal: weight-gradient scratch");
     if (wgrad_fast(a)) {
+        CFD_REQUIRE(a.P < (int64_t)1 << 31, CFD_ESHAPE, "weight gradient over 2^31 or more pixels");
         const float* act = nullptr;
         if (a.ss) {
             CFD_REQUIRE(a.act, CFD_ESTATE, "internal: activation scratch");
@@ -593,8 +615,8 @@ void launch_linear_wgrad(const float* d, const float* a, int B, int K, int N, in
 
 void launch_linear_dgrad(const float* d, const float* W, const float* x, int B, int K, int N, int act, int accumulate,
                          float* da, hipStream_t st) {
-    hipLaunchKernelGGL(linear_dgrad_kernel, dim3((unsigned)ceil_div((int64_t)B * K, 256)), dim3(256), 0, st, d, W, x,
-                       B, K, N, act, accumulate, da);
+    hipLaunchKernelGGL(linear_dgrad_kernel, dim3((unsigned)ceil_div(K, 32), B), dim3(256), 0, st, d, W, x, B, K, N,
+                       act, accumulate, da);
     check_launch("linear_dgrad_kernel");
 }
 

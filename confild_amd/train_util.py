@@ -250,7 +250,7 @@ class TrainLoop:
         self.logger.logkv_mean("grad_norm", float(torch.linalg.vector_norm(self.grad)))
         self.logger.logkv_mean("param_norm", float(torch.linalg.vector_norm(self.params)))
         self.opt.step(self.grad)
-        self.model.load_flat(self.params)
+        self.model.load_flat(self.params, alias=True)   # the module's tensors are views of the master buffer
 
     def _update_ema(self):
         lib = _lib.load()

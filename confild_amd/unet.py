@@ -406,11 +406,13 @@ class UNetModel(nn.Module):
         named = dict(self.named_parameters())
         return torch.cat([named[k].detach().reshape(-1).to(torch.float32) for k in self.param_keys()]).contiguous()
 
-    def load_flat(self, flat):
+    def load_flat(self, flat, alias=False):
         """Copy a flat_params()-ordered buffer back into the parameters.  On the
         handle's device the library re-packs from it on the GPU (cfd_unet_load_flat:
         one repack of every kernel layout, no host round trip); elsewhere the handle
-        re-packs on its next call."""
+        re-packs on its next call.  ``alias``: the parameters become views of
+        ``flat`` instead of copies (the training loop's master buffer: later
+        loads of the same buffer copy nothing)."""
         named = dict(self.named_parameters())
         keys = self.param_keys()
         n = sum(named[k].numel() for k in keys)
@@ -420,7 +422,12 @@ class UNetModel(nn.Module):
         with torch.no_grad():
             for k in keys:
                 p = named[k]
-                p.copy_(flat[o:o + p.numel()].reshape(p.shape))
+                view = flat[o:o + p.numel()].view(p.shape)
+                if alias and view.device == p.device and view.dtype == p.dtype:
+                    if p.data_ptr() != view.data_ptr():
+                        p.data = view
+                else:
+                    p.copy_(view)
                 o += p.numel()
         dev = flat.device
         entry = self._handles.get(dev.index) if dev.type == "cuda" else None
