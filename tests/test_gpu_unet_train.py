@@ -11,6 +11,7 @@ within 2e-4 of its max magnitude (the input-gradient test's bound), floored at
 are rounding noise on both sides; measured 5e-6 where none vanish, heads16).
 """
 import ast
+import os
 
 import numpy as np
 import pytest
@@ -23,6 +24,7 @@ from oracle import unet as ou
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 # 128 / 256 / 384 / 512 channels: every convolution of the weight-gradient walk on
@@ -212,3 +214,36 @@ def test_load_flat_device_repack_is_bitexact(hip, name):
     m.forward_tape(x, t)
     ref.forward_tape(x, t)
     assert torch.equal(m.param_grad(d), ref.param_grad(d))
+
+
+def test_trainloop_ddp_two_ranks(hip, tmp_path):
+    """Two TrainLoop ranks (one sample each, gloo over device tensors on the same
+    GPU): the flat gradient is averaged across the ranks (DistributedDataParallel),
+    so both ranks hold the same gradient, parameters and EMA bit for bit, and that
+    gradient is the single-process gradient of the two-sample batch (within the
+    parameter-gradient tolerance: B = 1 and B = 2 choose different split-K plans)."""
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "ddp")
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(HERE, "ddp_trainloop_worker.py"),
+           out]
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    r0 = torch.load(out + ".rank0.pt", weights_only=True)
+    r1 = torch.load(out + ".rank1.pt", weights_only=True)
+    for k in ("grad", "params", "ema"):
+        assert torch.equal(r0[k], r1[k]), k
+    g = golden("golden_unettrain.npz")
+    c = ast.literal_eval(str(g["case"]))
+    _, _, _, m = _unet(c["net"])
+    loop = _trainloop(c, m, [c["t"][0]])
+    loop.forward_backward(torch.from_numpy(g["x0"]).to(DEV), noise=torch.from_numpy(g["noise"][0]).to(DEV))
+    full = loop.grad.cpu()
+    assert float((r0["grad"] - full).abs().max()) <= 2e-4 * float(full.abs().max())
