@@ -1722,13 +1722,19 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
             q.splits = even_splits(nch, q.splits);
             return q;
         }
+        // at least CFD_CONV_KMIN (4) K tiles per split, at most CFD_CONV_SMAX (32)
+        // splits: the small levels (8^2, 4^2) run long K chains on few tiles, and
+        // at batch 1 each K tile waits a memory latency (config A 32^2 B=1 forward
+        // 2.78 -> 2.68 ms against 8 / 16; B=8 64^2 unchanged)
+        static const int kmin = env_int("CFD_CONV_KMIN", 4);
+        static const int smax = env_int("CFD_CONV_SMAX", 32);
         q.kx = mn >= 2048 ? 2 : 1;
         q.bm = q.kx == 2 ? 256 : 128;
         q.bn = 128;
         q.nw = q.kx == 2 ? 8 : 4;
         const int64_t t = ceil_div(mn, q.bm) * ceil_div(a.Cout, q.bn);
         q.splits = 1;
-        while (t * q.splits < 256 && nkt / (q.splits * 2) >= 8 && q.splits < 16) q.splits *= 2;
+        while (t * q.splits < 256 && nkt / (q.splits * 2) >= kmin && q.splits < smax) q.splits *= 2;
         while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
         return q;
     }
