@@ -6,6 +6,7 @@ bytes (FETCH_SIZE kB x 2 for gfx950 16-B reads, MI355X_MICROARCH.md)."""
 import collections
 import csv
 import glob
+import os
 import sys
 
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -15,7 +16,7 @@ for d in sys.argv[1:]:
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for x in csv.DictReader(open(f)):
             kn = x["Kernel_Name"]
-            if "conv" not in kn and "splitk" not in kn:
+            if not os.environ.get("PMC_ALL") and "conv" not in kn and "splitk" not in kn:
                 continue
             name = kn.replace("void ", "").replace("cfd::", "")
             name = name[:name.find("(")] if "(" in name else name
