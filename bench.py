@@ -129,13 +129,37 @@ def launch_ranks(n, argv):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
+    import time
     procs = []
     for r in range(n):
         env = dict(os.environ)
         env.update(rank_env(n, r, port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
-    rcs = [p.wait() for p in procs]
-    return next((rc for rc in rcs if rc), 0)
+    return wait_ranks(procs, time.sleep)
+
+
+def wait_ranks(procs, sleep):
+    """Poll every rank (as torchrun's agent does): the first one to exit non-zero
+    ends the job -- the others, which would otherwise sit in a rendezvous or a
+    collective until the backend timeout, are terminated (then killed) -- and its
+    code is returned; 0 once all have exited cleanly."""
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = next((rc for rc in rcs if rc not in (None, 0)), None)
+        if bad is not None:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=10)
+                except Exception:
+                    p.kill()
+                    p.wait()
+            return bad
+        if all(rc == 0 for rc in rcs):
+            return 0
+        sleep(0.2)
 
 
 def init_dist():
@@ -865,6 +889,19 @@ def main_dps(args, rank, world, dev):
     o["model"].check_finite(dev)
     steps_total = timed * args.steps
     its = steps_total * batch * world / elapsed
+    # counted FLOPs per chain-step (FlopCounterMode's convention, pinned in
+    # tests/test_host.py): U-Net forward with tape + its input-VJP (convolutions
+    # once more, both attention products twice) + the SIREN at the sensors,
+    # forward and backward to the latents
+    from confild_amd.nf_networks import latent_grad_flops
+    from confild_amd.unet import forward_flops
+    m = o["model"]
+    uf = forward_flops(m.image_size, m.in_channels, m.model_channels, m.out_channels, m.num_res_blocks,
+                       set(m.attention_resolutions), m.channel_mult, m.num_heads, m.num_head_channels)
+    d, L, co, nh, H = c["siren"]
+    sf = latent_grad_flops(d, L, co, nh, H, o["S"], 10)
+    per_chain = sum(uf.values()) + uf["conv"] + 2 * uf["attn"] + sf["forward"] + sf["backward"]
+    achieved = per_chain * steps_total * batch / (elapsed * 1e12)   # per GPU
     if rank == 0:
         rec = {"metric": "guided DPS reverse steps/sec (it/s summed over chains), Case4 conditional",
                "value": its, "unit": "it/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -878,6 +915,16 @@ def main_dps(args, rank, world, dev):
                "reference_published": ("9.26-9.35 it/s at one chain, unstated NVIDIA GPU "
                                        "(inference_phy_random_sensor.ipynb:321-330)") if args.config == "Case4" else None,
                "per_chain_it_s": its / (batch * world),
+               "roofline": {"bound": "mfma", "kernel": "whole guided step (U-Net forward with tape + input-VJP on "
+                                                       "split-f16 MFMA, SIREN tape on fp32 MFMA, step kernels)",
+                            "achieved": achieved, "peak": F16_PEAK_TFLOPS / 3,
+                            "peak_basis": "f16 dense MFMA peak / 3 (split-f16 convolutions)", "unit": "TFLOP/s",
+                            "frac": achieved / (F16_PEAK_TFLOPS / 3),
+                            "peak_sustained": F16_SUSTAINED_TFLOPS / 3,
+                            "frac_sustained": achieved / (F16_SUSTAINED_TFLOPS / 3), "traffic": None,
+                            "flops_per_chain_step": per_chain,
+                            "flops_split": {"unet_forward": sum(uf.values()), "unet_input_vjp": uf["conv"] + 2 * uf["attn"],
+                                            "siren_forward": sf["forward"], "siren_backward": sf["backward"]}},
                "cpu_baseline": None if args.no_cpu_baseline or world > 1 else cpu_baseline(args.config),
                "rccl_ranks": world}
         print(json.dumps(rec), flush=True)

@@ -63,9 +63,13 @@ class Adam:
                 state[i] = {"step": torch.tensor(float(self.steps)),
                             "exp_avg": self.exp_avg[o:o + n].reshape(shp).clone(),
                             "exp_avg_sq": self.exp_avg_sq[o:o + n].reshape(shp).clone()}
+        # decoupled_weight_decay: torch >= 2.9 defines AdamW as Adam with it set, and
+        # Adam.__setstate__ defaults a missing key to False (L2-coupled decay) -- so
+        # the key is written, True for the decoupled update this optimizer runs
         group = {"lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.weight_decay,
                  "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
-                 "differentiable": False, "fused": None, "params": list(range(len(spans)))}
+                 "differentiable": False, "fused": None, "decoupled_weight_decay": self.weight_decay > 0,
+                 "params": list(range(len(spans)))}
         return {"state": state, "param_groups": [group]}
 
     def load_torch_state_dict(self, sd, spans):
@@ -74,15 +78,25 @@ class Adam:
         if len(groups) != 1 or len(groups[0]["params"]) != len(spans):
             raise ValueError("optimizer state has a different parameter layout")
         g = groups[0]
+        wd = float(g.get("weight_decay", 0.0))
+        if wd > 0 and not g.get("decoupled_weight_decay", True):
+            raise ValueError("optimizer state is L2-coupled Adam (decoupled_weight_decay False); "
+                             "cfd_adam_step runs the decoupled (AdamW) update")
         self.lr, self.betas, self.eps = float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"])
-        self.weight_decay = float(g.get("weight_decay", 0.0))
+        self.weight_decay = wd
         steps = set()
         for i, (o, shp) in enumerate(spans):
             st = sd["state"].get(i, sd["state"].get(str(i)))
             if st is None:
                 steps.add(0)
                 continue
-            n = st["exp_avg"].numel()
+            n = 1
+            for d in shp:
+                n *= d
+            for key in ("exp_avg", "exp_avg_sq"):
+                if tuple(st[key].shape) != tuple(shp):
+                    raise ValueError(f"optimizer state {key} of parameter {i} has shape {tuple(st[key].shape)}, "
+                                     f"the parameter {tuple(shp)}")
             self.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
             self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
             steps.add(int(float(st["step"])))
@@ -93,14 +107,15 @@ class Adam:
 
 def _batches(n, batch_size, shuffle, world_size, rank, epoch, generator=None):
     """The reference's DataLoader index order: RandomSampler / SequentialSampler
-    (world_size 1) or DistributedSampler(shuffle=False) with set_epoch."""
+    (world_size 1) or ``DistributedSampler(dataset)`` -- its defaults, shuffle=True
+    and seed 0, reshuffled per epoch by ``set_epoch`` (train.py:360-365,398)."""
     from torch.utils.data import BatchSampler, DistributedSampler, RandomSampler, SequentialSampler
     # a DataLoader iterator draws its worker base seed from the RNG first
     # (torch.utils.data.dataloader._BaseDataLoaderIter), then the sampler its own
     torch.empty((), dtype=torch.int64).random_(generator=generator)
     idx = range(n)
     if world_size > 1:
-        s = DistributedSampler(idx, num_replicas=world_size, rank=rank, shuffle=False)
+        s = DistributedSampler(idx, num_replicas=world_size, rank=rank)
         s.set_epoch(epoch)
     else:
         s = RandomSampler(idx, generator=generator) if shuffle else SequentialSampler(idx)

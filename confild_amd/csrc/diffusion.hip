@@ -351,31 +351,41 @@ extern "C" int cfd_dps_update(const float* sample, const float* g_direct, const 
 }
 
 // ---------------------------------------------------------------------------
-// Adam / AdamW (torch.optim.Adam, torch/optim/adam.py _single_tensor_adam, fp32,
-// amsgrad off; weight_decay > 0 is AdamW's decoupled decay, param *= 1 - lr wd,
-// first): the optimisers of the CNF training loop (N/scripts/train.py:385-416)
-// and of the diffusion TrainLoop (AdamW, U/src/train_util.py:78-80).  Per
-// element, in torch's operation order:
-//   exp_avg.lerp_(grad, 1 - beta1)                  (ATen lerp's two-branch form)
+// Adam / AdamW (torch.optim.Adam / AdamW, fp32, amsgrad off; weight_decay > 0 is
+// AdamW's decoupled decay, param *= 1 - lr wd, first): the optimisers of the CNF
+// training loop (N/scripts/train.py:385-416) and of the diffusion TrainLoop (AdamW,
+// U/src/train_util.py:78-80).  The reference steps them on its GPU, where torch's
+// default is the multi-tensor (foreach) path of torch/optim/adam.py; per element,
+// in that path's operation order and with the fused multiply-adds its device
+// kernels execute (pinned bit for bit against torch.optim.AdamW on the MI355X by
+// tests/test_gpu_optim.py; the probe is tools/dev/optim_probe.py):
+//   exp_avg.lerp_(grad, 1 - beta1)          w < 0.5: fma(w, g - m, m)
+//                                           else:    fma(-(g - m), 1 - w, g)
 //   exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
-//   denom = exp_avg_sq.sqrt() / sqrt(1 - beta2^step) + eps
+//                                           fma(1 - beta2, g * g, v * beta2)
+//   denom = exp_avg_sq.sqrt() / sqrt(1 - beta2^step) + eps   (IEEE sqrt, division)
 //   param.addcdiv_(exp_avg, denom, value=-lr / (1 - beta1^step))
+//                                           fma(-step_size, m / denom, p)
 // The step-dependent scalars are formed in double on the host as torch does.
+// torch's CPU kernels differ in two places (addcmul as fma(value * g, g, v),
+// addcdiv as p + (value * m) / denom, and a vectorised sqrt that is not always
+// correctly rounded): within an ulp of this on the same inputs.
 // ---------------------------------------------------------------------------
 namespace cfd {
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, int64_t n, float w1, float beta2, float w2, float bc2s, float eps,
                             float neg_step, float decay) {
+#pragma clang fp contract(off)
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (decay != 1.0f) p[i] = p[i] * decay;   // AdamW: param.mul_(1 - lr * weight_decay) first
+    float pi = p[i];
+    if (decay != 1.0f) pi = pi * decay;   // AdamW: param.mul_(1 - lr * weight_decay) first
     const float gi = g[i];
     float mi = m[i];
-    mi = w1 < 0.5f ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
-    float vi = v[i] * beta2;
-    vi = vi + w2 * gi * gi;
+    mi = w1 < 0.5f ? __builtin_fmaf(w1, gi - mi, mi) : __builtin_fmaf(-(gi - mi), 1.0f - w1, gi);
+    const float vi = __builtin_fmaf(w2, gi * gi, v[i] * beta2);
     const float denom = sqrtf(vi) / bc2s + eps;
-    p[i] = p[i] + neg_step * (mi / denom);
+    p[i] = __builtin_fmaf(neg_step, mi / denom, pi);
     m[i] = mi;
     v[i] = vi;
 }

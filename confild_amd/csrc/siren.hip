@@ -1643,11 +1643,20 @@ TrainWs train_ws(const cfd_siren* h, int64_t N, int R, void* base) {
     return w;
 }
 
+// the latent-gradient GEMM (launch_gemm_f32) needs these; checked before any
+// launch so an unsupported configuration leaves the caller's sums untouched
+void train_shape_check(const cfd_siren* h) {
+    const int64_t nf = (int64_t)(h->cfg.num_hidden_layers + 1) * h->cfg.hidden_features;
+    CFD_REQUIRE(h->cfg.in_latent_features % 4 == 0 && nf % 16 == 0, CFD_ESHAPE,
+                "training needs in_latent_features % 4 == 0 and (nh+1)*H % 16 == 0");
+}
+
 }  // namespace
 
 extern "C" int cfd_siren_train_workspace_bytes(const cfd_siren* h, int64_t N, int R, size_t* bytes) {
     return cfd::guard([&] {
         CFD_REQUIRE(h && bytes && N >= 0 && R >= 0, CFD_EARG, "bad argument");
+        train_shape_check(h);
         *bytes = sizeof(float) * train_ws(h, N, R, nullptr).floats;
     });
 }
@@ -1660,6 +1669,7 @@ extern "C" int cfd_siren_train_grad(cfd_siren* h, const float* coords, int64_t N
                     "null argument");
         CFD_REQUIRE(N >= 1 && N <= (1 << 20) && R >= 1, CFD_EARG, "bad coordinate / row count");
         CFD_REQUIRE(((uintptr_t)ws & 15) == 0, CFD_EARG, "workspace must be 16-byte aligned");
+        train_shape_check(h);
         for (const auto& p : h->params) CFD_REQUIRE(p.set, CFD_ESTATE, "SIREN parameter not set: " + p.key);
         const TrainWs w = train_ws(h, N, R, ws);
         CFD_REQUIRE(ws_bytes >= sizeof(float) * w.floats, CFD_EARG, "workspace too small");
@@ -1717,11 +1727,7 @@ extern "C" int cfd_siren_train_grad(cfd_siren* h, const float* coords, int64_t N
             }
         }
         // latent rows: g_z = sum_i D_i V_i, added into grad_latents[rows]
-        if (L % 4 == 0 && nf % 16 == 0) {
-            cfd::launch_gemm_f32(false, w.D, (int)nf, h->V, L, nullptr, w.gz, L, R, L, (int)nf, st, w.gpart);
-        } else {
-            CFD_REQUIRE(false, CFD_ESHAPE, "training needs in_latent_features % 4 == 0 and (nh+1)*H % 16 == 0");
-        }
+        cfd::launch_gemm_f32(false, w.D, (int)nf, h->V, L, nullptr, w.gz, L, R, L, (int)nf, st, w.gpart);
         hipLaunchKernelGGL(cfd::scatter_add_rows_kernel, dim3((unsigned)cfd::ceil_div((int64_t)R * L, 256)),
                            dim3(256), 0, st, w.gz, rows, grad_latents, R, L);
         cfd::check_launch("scatter_add_rows_kernel");

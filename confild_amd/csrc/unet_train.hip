@@ -469,8 +469,11 @@ __global__ __launch_bounds__(256) void linear_dgrad_kernel(const float* __restri
 // update_ema: targ = targ * rate + src * (1 - rate)  (targ.mul_(rate).add_(src, alpha=1 - rate))
 __global__ void ema_kernel(float* __restrict__ targ, const float* __restrict__ src, int64_t n, float rate,
                            float omr) {
+#pragma clang fp contract(off)
+    // update_ema's targ.mul_(rate).add_(src, alpha=1 - rate): torch's add-with-alpha
+    // is one fused multiply-add on the rounded product (GPU and CPU kernels alike)
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) targ[i] = targ[i] * rate + src[i] * omr;
+    if (i < n) targ[i] = __builtin_fmaf(src[i], omr, targ[i] * rate);
 }
 
 // diffusion training loss (GaussianDiffusion.training_losses, MSE on eps,

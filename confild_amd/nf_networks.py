@@ -39,6 +39,22 @@ def _first_layer_sine_init(m):
         m.weight.uniform_(-1 / n, 1 / n)                                     # initialization.py:127-132
 
 
+def latent_grad_flops(d, L, c, nh, H, rows, points):
+    """FLOPs of the DPS operator's SIREN part as FlopCounterMode counts the
+    reference (measurements.py:219-226 under condition_methods.py:31-47): the
+    forward at ``rows`` latent rows x ``points`` sensor coordinates -- the FiLM
+    products (nh + 1) x (L -> H) per row, the first coordinate layer once per
+    point (the reference broadcasts it over the rows), 2(nh H^2 + Hc) per (row,
+    point) pair -- and autograd's backward to the latents only: every hidden and the
+    output layer's input-gradient per pair, and the FiLM products' latent gradient
+    per row.  Returns {"forward", "backward"}.  Pinned against FlopCounterMode on
+    the CPU oracle (tests/test_host.py)."""
+    film = 2 * (nh + 1) * H * L * rows
+    fwd = 2 * d * H * points + 2 * (nh * H * H + H * c) * rows * points + film
+    bwd = 2 * (nh * H * H + H * c) * rows * points + film
+    return {"forward": fwd, "backward": bwd}
+
+
 class SIRENAutodecoder_film(nn.Module):
     """Constructor as nf_networks.py:447-478 (sine nonlinearity, no premap)."""
 

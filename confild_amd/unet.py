@@ -104,6 +104,62 @@ def param_shapes(in_channels, model_channels, out_channels, num_res_blocks, atte
     return s
 
 
+def forward_flops(image_size, in_channels, model_channels, out_channels, num_res_blocks, attention_resolutions,
+                  channel_mult, num_heads=1, num_head_channels=-1):
+    """FLOPs of one sample's forward, counted as torch's FlopCounterMode counts the
+    reference (2 x MAC of every convolution, bmm / einsum and addmm; GroupNorm,
+    SiLU and adds are not counted), by the walk of param_shapes / unet.py:469-663.
+    Returns {"conv", "attn", "linear"}: the 2-D and 1-D convolutions, the two
+    attention products (4 T^2 C per block), and time_embed + every emb_layers.
+    Pinned against FlopCounterMode on the CPU oracle (tests/test_host.py)."""
+    mc, tdim = model_channels, model_channels * 4
+    f = {"conv": 0, "attn": 0, "linear": 2 * (mc * tdim + tdim * tdim)}
+    hw = image_size * image_size
+
+    def res(cin, cout, px):
+        f["conv"] += 2 * px * cout * cin * 9 + 2 * px * cout * cout * 9 + (2 * px * cout * cin if cin != cout else 0)
+        f["linear"] += 2 * tdim * cout
+
+    def attn(c, px):
+        f["conv"] += 2 * px * 3 * c * c + 2 * px * c * c
+        f["attn"] += 4 * px * px * c
+
+    ch = int(channel_mult[0] * mc)
+    f["conv"] += 2 * hw * ch * in_channels * 9
+    chans, ds, px = [ch], 1, hw
+    for level, mult in enumerate(channel_mult):
+        for _ in range(num_res_blocks):
+            cout = int(mult * mc)
+            res(ch, cout, px)
+            ch = cout
+            if ds in attention_resolutions:
+                attn(ch, px)
+            chans.append(ch)
+        if level != len(channel_mult) - 1:
+            px_out = ((image_size // ds + 1) // 2) ** 2
+            f["conv"] += 2 * px_out * ch * ch * 9
+            chans.append(ch)
+            ds *= 2
+            px = px_out
+    res(ch, ch, px)
+    attn(ch, px)
+    res(ch, ch, px)
+    for level, mult in list(enumerate(channel_mult))[::-1]:
+        for i in range(num_res_blocks + 1):
+            ich = chans.pop()
+            cout = int(mc * mult)
+            res(ch + ich, cout, px)
+            ch = cout
+            if ds in attention_resolutions:
+                attn(ch, px)
+            if level and i == num_res_blocks:
+                px *= 4
+                f["conv"] += 2 * px * ch * ch * 9
+                ds //= 2
+    f["conv"] += 2 * px * out_channels * ch * 9
+    return f
+
+
 def _zero_init_keys(keys):
     """Modules the reference wraps in zero_module (unet.py:210-212,294,615)."""
     out = set()

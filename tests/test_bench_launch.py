@@ -27,3 +27,19 @@ def test_bench_rejects_gpus_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--launch-check"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_wait_ranks_fails_fast_and_stops_the_others():
+    """A rank that exits non-zero ends the job: the ranks still running (here a
+    sleeping child standing in for one blocked in a rendezvous) are terminated and
+    the failing code is returned, instead of waiting for the backend timeout."""
+    import time
+    sys.path.insert(0, ROOT)
+    import bench
+    hang = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(600)"])
+    fail = subprocess.Popen([sys.executable, "-c", "import sys; sys.exit(7)"])
+    t0 = time.time()
+    assert bench.wait_ranks([hang, fail], time.sleep) == 7
+    assert time.time() - t0 < 60 and hang.poll() is not None
+    ok = [subprocess.Popen([sys.executable, "-c", "pass"]) for _ in range(2)]
+    assert bench.wait_ranks(ok, time.sleep) == 0

@@ -204,6 +204,32 @@ def test_configD_dps_steps_at_config_widths(hip):
         assert max(e.values()) <= 2e-5 and ed <= 1e-5, (idx, e, ed)
 
 
+def test_configD_batched_chains_equal_single_chains(hip):
+    """Config D as the bench runs it -- 8 chains per GPU of the 64^2 guided U-Net
+    with SIREN(3, 64, 3, 15, 384) at 10 sensors, the whole 256-step 'ps' loop --
+    equals the 8 chains run one by one, bit for bit (sample and per-step residual
+    norm): a chain's arithmetic does not depend on the batch it runs in, so the
+    chains shard over GPUs with no collective (tiny16 version: test_gpu_dps.py)."""
+    from confild_amd.guided.unet import create_model as guided_model
+    c = DPS_D
+    g = golden("golden_dpsD.npz")
+    model = _unet(c, guided_model)
+    op = _operator_D(g)
+    cond, sampler = _guided(c["respacing"], op, c["scale"])
+    y = torch.from_numpy(g["measurement"]).to(DEV)
+    S, L = c["unet"]["image_size"], c["siren"][1]
+    xs = torch.from_numpy(synth.normal(c["siren_seed"], "dpsD/batched_xs", (8, 1, S, L))).to(DEV)
+    full = sampler.p_sample_loop(model=model, x_start=xs, measurement=y, measurement_cond_fn=cond.conditioning,
+                                 seed=2024)
+    dfull = sampler.distances.clone()
+    assert torch.isfinite(full).all() and dfull.shape[1] == 8
+    for s in range(8):
+        one = sampler.p_sample_loop(model=model, x_start=xs[s:s + 1], measurement=y,
+                                    measurement_cond_fn=cond.conditioning, seed=2024, sample_offset=s)
+        assert torch.equal(one, full[s:s + 1]), s
+        assert torch.equal(sampler.distances[:, 0], dfull[:, s]), s
+
+
 def _case4_operator(tmp):
     from confild_amd.guided.measurements import get_operator
     paths = case4_files(str(tmp))

@@ -136,12 +136,38 @@ def test_trainloop_matches_reference_run(hip, tmp_path):
     _, cfg, sd, m = _unet(c["net"])
     loop = _trainloop(c, m, c["t"], log_dir=str(tmp_path))
     x0 = torch.from_numpy(g["x0"]).to(DEV)
-    losses, first = [], None
+    losses, first, grads = [], None, []
+    p_start = loop.params.clone()
     for k in range(c["steps"]):
         loop.run_step(x0, None, None, noise=torch.from_numpy(g["noise"][k]).to(DEV))
+        grads.append(loop.grad.clone())
         if first is None:
             first = _unpack(loop, loop.grad)
         losses.append(loop.logger.dumpkvs()["loss"])
+    # the optimiser and EMA on our own gradients are the reference's bit for bit:
+    # torch.optim.AdamW (its GPU default, foreach) over the per-parameter tensors and
+    # update_ema (nn.py:71-80) replayed from the same start -- so what the parameter
+    # bound below still allows is the propagation of the gradients' rounding alone
+    named = dict(m.named_parameters())
+    views, o = [], 0
+    rp = p_start.clone()
+    for k in loop.keys:
+        n = named[k].numel()
+        views.append(rp[o:o + n].view(named[k].shape))
+        o += n
+    tparams = [v.clone().requires_grad_(True) for v in views]
+    topt = torch.optim.AdamW(tparams, lr=c["lr"], weight_decay=c["weight_decay"])
+    tema = [t.detach().clone() for t in tparams]
+    for gk in grads:
+        o = 0
+        for t in tparams:
+            t.grad = gk[o:o + t.numel()].view(t.shape).clone()
+            o += t.numel()
+        topt.step()
+        for targ, src in zip(tema, tparams):
+            targ.mul_(c["ema_rate"]).add_(src.detach(), alpha=1 - c["ema_rate"])
+    assert torch.equal(torch.cat([t.detach().reshape(-1) for t in tparams]), loop.params)
+    assert torch.equal(torch.cat([t.reshape(-1) for t in tema]), loop.ema_params[0])
     names = [str(n) for n in g["names"]]
     rep = check(g, c, names, losses, first, _unpack(loop, loop.params), _unpack(loop, loop.ema_params[0]),
                 rtol_loss0=2e-5, rtol_loss1=1e-4, tol_grad=2e-4, atol_grad=5e-6, tol_param=1e-4,

@@ -271,11 +271,36 @@ def test_cnf_train_batch_order_is_the_dataloaders(shuffle):
         assert _batches(11, 4, shuffle, 1, 0, epoch) == want
 
 
-def test_cnf_train_distributed_batches_partition_the_samples():
-    """world_size > 1: DistributedSampler(shuffle=False) shards (train.py:361-372)."""
+def test_cnf_train_distributed_batches_are_the_reference_loaders():
+    """world_size > 1: the reference's ``DataLoader(dataset, shuffle=False,
+    sampler=DistributedSampler(dataset))`` (train.py:360-365) -- the sampler's
+    default shuffle=True, seed 0 -- with ``set_epoch(i)`` each epoch (train.py:398):
+    a different random shard per rank and epoch, together a partition."""
+    from torch.utils.data import DataLoader, Dataset, DistributedSampler
     from confild_amd.cnf_train import _batches
-    got = sorted(i for r in range(2) for b in _batches(10, 3, False, 2, r, 0) for i in b)
-    assert got == list(range(10))
+
+    class _Idx(Dataset):
+        def __len__(self):
+            return 10
+
+        def __getitem__(self, i):
+            return i
+
+    seen = []
+    for epoch in range(3):
+        got_all = []
+        for r in range(2):
+            sampler = DistributedSampler(_Idx(), num_replicas=2, rank=r)
+            sampler.set_epoch(epoch)
+            torch.manual_seed(11 + epoch)
+            want = [b.tolist() for b in DataLoader(_Idx(), batch_size=3, shuffle=False, sampler=sampler)]
+            torch.manual_seed(11 + epoch)
+            got = _batches(10, 3, False, 2, r, epoch)
+            assert got == want
+            got_all += [i for b in got for i in b]
+        assert sorted(got_all) == list(range(10))
+        seen.append(got_all)
+    assert seen[0] != seen[1], "set_epoch must reshuffle the shards"
 
 
 def test_schedule_samplers_match_reference_draws():
@@ -319,3 +344,48 @@ def test_trainloop_host_side():
         TrainLoop(**kw, use_fp16=True)
     with pytest.raises(_lib.CfdError):
         TrainLoop(**kw)                      # a CPU model: the loop runs on the GPU only
+
+
+@pytest.mark.parametrize("case", ["tiny", "cfgA32", "cfgB64"])
+def test_flop_counts_match_flopcounter_on_the_oracle(case):
+    """confild_amd.unet.forward_flops (the bench's roofline numerator) equals
+    torch's FlopCounterMode over the oracle forward, and forward conv + 2 x
+    attention equals its count of the input-gradient (autograd.grad to x: the
+    DPS adjoint); nf_networks.latent_grad_flops equals FlopCounterMode over the
+    oracle SIREN forward and its gradient to the latents."""
+    from torch.utils.flop_counter import FlopCounterMode
+
+    from confild_amd import synth
+    from confild_amd.nf_networks import latent_grad_flops
+    from confild_amd.unet import forward_flops
+    from oracle import siren as osn
+    from oracle import unet as ou
+    kw = {"tiny": dict(image_size=16, num_channels=32, num_res_blocks=1, channel_mult="1,2", num_heads=2,
+                       num_head_channels=16, attention_resolutions="8"),
+          "cfgA32": dict(image_size=32, num_channels=128, num_res_blocks=2, channel_mult="1,2,3,4", num_heads=4,
+                         num_head_channels=64, attention_resolutions="32,16,8"),
+          "cfgB64": dict(image_size=64, num_channels=128, num_res_blocks=2, channel_mult="", num_heads=4,
+                         num_head_channels=64, attention_resolutions="32,16,8")}[case]
+    cfg = ou.Config(**kw)
+    sd = {k: torch.from_numpy(v) for k, v in synth.unet_state_dict(1, ou.param_shapes(cfg)).items()}
+    S = kw["image_size"]
+    x = torch.randn(1, 1, S, S, requires_grad=True)
+    with FlopCounterMode(display=False) as fc:
+        eps = ou.forward(sd, cfg, x, torch.tensor([10]))
+    with FlopCounterMode(display=False) as fc2:
+        torch.autograd.grad(eps, x, torch.randn_like(eps))
+    f = forward_flops(S, 1, cfg.model_channels, 1, cfg.num_res_blocks, set(cfg.attention_ds), cfg.channel_mult,
+                      cfg.num_heads, cfg.num_head_channels)
+    assert sum(f.values()) == fc.get_total_flops()
+    assert f["conv"] + 2 * f["attn"] == fc2.get_total_flops()
+    if case == "cfgB64":
+        assert sum(f.values()) == 68_614_488_064     # SURVEY 8d: 68.61 GF per sample
+    d, L, c, nh, H = 3, 64, 3, 15, 384
+    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1, d, L, c, nh, H).items()}
+    z = torch.randn(5, 1, L, requires_grad=True)
+    with FlopCounterMode(display=False) as fs:
+        y = osn.forward(ssd, torch.rand(1, 10, d), z)
+    with FlopCounterMode(display=False) as fs2:
+        torch.autograd.grad(y, z, torch.randn_like(y))
+    assert latent_grad_flops(d, L, c, nh, H, 5, 10) == {"forward": fs.get_total_flops(),
+                                                         "backward": fs2.get_total_flops()}
