@@ -25,6 +25,10 @@ TRAJ_E = dict(tag="trajE", seed=1234, image_size=128, segments=((999, 20), (19, 
               unet=dict(image_size=128, num_channels=128, num_res_blocks=2, channel_mult=None, num_heads=4,
                         num_head_channels=64, attention_resolutions="32,16,8"))
 
+# config E, a longer stretch (round 4): 100 consecutive steps of the same loop
+# (indices 599..500), so the bf16 operands' drift is stated over 100 steps
+TRAJ_E100 = dict(tag="trajE100", start=599, n=100, keep=tuple(range(0, 100, 10)) + (99,))
+
 # config A (configs[0]): Case1 uncond 32^2 mult (1,2,3,4), DDIM-50, 1k-coord decode
 CFG_A = dict(tag="cfgA", seed=1234, image_size=32, respacing="ddim50", vmax=1.5, vmin=-1.5,
              unet=dict(image_size=32, num_channels=128, num_res_blocks=2, channel_mult="1,2,3,4", num_heads=4,

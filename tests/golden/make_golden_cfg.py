@@ -21,6 +21,8 @@ Fixtures
   * golden_trajE.npz  -- config E: two 20-step segments (indices 999..980 and
     19..0) of the 1000-step DDPM loop of the 128x128 default-mult U-Net at
     B = 1 through the reference's p_sample, sample and x0_hat per step;
+  * golden_trajE100.npz -- config E: 100 consecutive steps (indices 599..500)
+    of the same loop, sample and x0_hat every 10 steps and at the end;
   * golden_case4steps.npz -- the real Case4 loop: 10 consecutive DDPM + 'ps'
     steps (indices 500..491) at 384^2: per step the residual norm, image and
     x0_hat on a 4x-strided subgrid and whole-image checksums; the final image;
@@ -65,7 +67,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from confild_amd import synth  # noqa: E402
-from cfg_cases import (CASE4_OP, CASE4_STEPS, CFG_A, CNF_INF, DPS_D, POST, TRAJ_B, TRAJ_E, case4_files,  # noqa: E402
+from cfg_cases import (CASE4_OP, CASE4_STEPS, CFG_A, CNF_INF, DPS_D, POST, TRAJ_B, TRAJ_E, TRAJ_E100,  # noqa: E402
+                       case4_files,
                        cnf_inference_coords, cnf_inference_files, noise_for, post_inputs, unet_weights)
 
 torch.set_num_threads(8)
@@ -154,6 +157,30 @@ def gen_trajE():
         out_arrays[f"pred_xstart{start}"] = np.stack([x0s[k] for k in keep])
     print(f"trajE: {sum(n for _, n in c['segments'])} steps in {time.time() - t0:.1f} s")
     _save("golden_trajE.npz", keep=np.array(c["keep"], dtype=np.int64), **out_arrays)
+
+
+def gen_trajE100():
+    """config E: 100 consecutive steps (599..500) of the 1000-step DDPM loop of the
+    128^2 U-Net through the reference's p_sample, B = 1, from a seeded x."""
+    from src.script_util import create_gaussian_diffusion
+    c = TRAJ_E100
+    m = _ref_unet(TRAJ_E["unet"], TRAJ_E["seed"])
+    diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="")
+    S = TRAJ_E["image_size"]
+    shape = (1, 1, S, S)
+    x = torch.from_numpy(noise_for(f"{c['tag']}/x", 0, shape))
+    samples, x0s = [], []
+    t0 = time.time()
+    with _Noise(f"{c['tag']}/steps"), torch.no_grad():
+        for i in range(c["start"], c["start"] - c["n"], -1):
+            out = diff.p_sample(m, x, torch.tensor([i]), clip_denoised=True)
+            x = out["sample"]
+            samples.append(x.numpy())
+            x0s.append(out["pred_xstart"].numpy())
+    print(f"trajE100: {c['n']} steps in {time.time() - t0:.1f} s")
+    keep = list(c["keep"])
+    _save("golden_trajE100.npz", keep=np.array(keep, dtype=np.int64), samples=np.stack([samples[k] for k in keep]),
+          pred_xstart=np.stack([x0s[k] for k in keep]))
 
 
 # ---------------------------------------------------------------------------
@@ -396,7 +423,7 @@ def gen_post():
     _save("golden_post.npz", frames=frames.astype(np.float32), nan_frame=nanf.astype(np.float32))
 
 
-GEN = {"trajB": gen_trajB, "trajE": gen_trajE, "case4steps": gen_case4steps, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps,
+GEN = {"trajB": gen_trajB, "trajE": gen_trajE, "trajE100": gen_trajE100, "case4steps": gen_case4steps, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps,
        "cnfinf": gen_cnfinf, "post": gen_post}
 
 if __name__ == "__main__":

@@ -287,6 +287,32 @@ def test_oracle_configE_segment_prefix():
                     assert np.abs(x0.numpy() - g[f"pred_xstart{start}"][j]).max() < 2e-5 * amp, (start, k)
 
 
+def test_oracle_configE_100_step_fixture_prefix():
+    """The first 11 steps (keep indices 0 and 10) of the 100-step config-E
+    fixture (indices 599..500) through the oracle: bit-level agreement with the
+    reference's own run pins the fixture the GPU drift test reads."""
+    cc = _cfg_cases()
+    c, ce = cc.TRAJ_E100, cc.TRAJ_E
+    g = golden("golden_trajE100.npz")
+    cfg = ou.Config(**ce["unet"])
+    sd = {k: torch.from_numpy(v) for k, v in cc.unet_weights(ou.param_shapes(cfg), ce["seed"]).items()}
+    tb = od.Tables(1000, "cosine", "")
+    S = ce["image_size"]
+    shape = (1, 1, S, S)
+    keep = [int(k) for k in g["keep"]]
+    with torch.no_grad():
+        x = torch.from_numpy(cc.noise_for(f"{c['tag']}/x", 0, shape))
+        for k, i in enumerate(range(c["start"], c["start"] - 11, -1)):
+            t = torch.full((1,), i, dtype=torch.int64)
+            eps = ou.forward(sd, cfg, x, t)
+            x, x0 = od.ddpm_step(tb, x, t, eps, torch.from_numpy(cc.noise_for(f"{c['tag']}/steps", k, shape)))
+            if k in keep:
+                j = keep.index(k)
+                assert np.abs(x.numpy() - g["samples"][j]).max() < 2e-5, k
+                amp = max(1.0, float(tb.sqrt_recipm1_alphas_cumprod[i]))
+                assert np.abs(x0.numpy() - g["pred_xstart"][j]).max() < 2e-5 * amp, k
+
+
 def test_oracle_case4_chain_first_step(tmp_path):
     """The first step of the real-Case4 10-step chain fixture (384^2 U-Net, the
     file-built operator) through the oracle's autograd DPS step."""
