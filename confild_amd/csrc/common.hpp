@@ -25,6 +25,30 @@
 #define CFD_DASSERT(cond) ((void)0)
 #endif
 
+// In-kernel timestamps of the development build (make STAMPS=1 ->
+// lib/libconfild_hip_stamps.so; tools/dev/stamps.py): wave 0 of a workgroup
+// records (realtime, kind/launch/slot, block, shader clock) at named points of
+// the small-batch kernels into a buffer set by cfd_stamps_set.  Vector atomics
+// and vector stores only.  Compiled out of the shipped library.
+#ifdef CFD_STAMPS
+__device__ __forceinline__ void cfd_stamp(unsigned long long* buf, unsigned kind, unsigned seq, unsigned slot) {
+    if (buf && threadIdx.x == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long i = atomicAdd(buf, 1ULL);
+        if (i < (1ull << 20)) {
+            unsigned long long* r = buf + 8 + 4 * i;
+            r[0] = t;
+            r[1] = ((unsigned long long)kind << 56) | ((unsigned long long)seq << 24) | slot;
+            r[2] = blockIdx.x + ((unsigned long long)blockIdx.y << 20) + ((unsigned long long)blockIdx.z << 40);
+            r[3] = __builtin_amdgcn_s_memtime();
+        }
+    }
+}
+#define CFD_STAMP(buf, kind, seq, slot) cfd_stamp(buf, kind, seq, slot)
+#else
+#define CFD_STAMP(buf, kind, seq, slot) ((void)0)
+#endif
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

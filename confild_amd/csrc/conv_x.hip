@@ -23,6 +23,7 @@
 // (ds_read_b128, lanes 0-31 rows 0-31 chunk 2s, lanes 32-63 chunk 2s+1) then
 // covers the 64 banks once; the 8-B staging writes stay conflict-free.
 #include <algorithm>
+#include <type_traits>
 
 #include "unet_kernels.hpp"
 
@@ -61,6 +62,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     constexpr int STAGE = 2 * ABYTES + 2 * BBYTES;                 // A hi, A lo, B hi, B lo
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
+    CFD_STAMP(a.stamps, 2, a.seq, 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kg = wave / (WGM * WGN), wrem = wave % (WGM * WGN);
@@ -245,6 +247,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
         }
         store_tile(0, 0);
         __syncthreads();
+        CFD_STAMP(a.stamps, 2, a.seq, 2);
         if constexpr (PF == 1) {
             int cur = 0;
             for (int kt = kt0; kt < kt1; kt += KG) {
@@ -259,6 +262,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
         }
     }
 
+    CFD_STAMP(a.stamps, 2, a.seq, 3);
     // combine the K groups through LDS: groups 1.. park their sums, group 0 adds
     // them in group order (fixed summation order)
     if constexpr (KG > 1) {
@@ -317,6 +321,10 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
                     if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][e];
                 }
             }
+#ifdef CFD_STAMPS
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
+        CFD_STAMP(a.stamps, 2, a.seq, 4);
         return;
     }
 #pragma unroll
@@ -371,8 +379,14 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // BF (config E, K1hb): bf16 operands -- the halo rounded to bf16 (RNE) as it is
 // staged, weights from the bf16 arena (a.wbf, a.wlo null) -- one
 // v_mfma_f32_32x32x16_bf16 per product, one halo plane and one weight plane.
-template <int BM, int TW, int KG = 1, bool BF = false>
+// SB (with BF; a.src_bf16): the source already holds those bf16 values (a
+// GroupNorm's out_bf16 output, rounded by the same conversion): 8-byte halo
+// pieces (4 channels of 2 bytes, byte offset 2 * (pixel * C + channel)) are
+// copied to LDS as they are -- half the activation bytes, the same bits.
+template <int BM, int TW, int KG = 1, bool BF = false, bool SB = false>
 __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
+    static_assert(!SB || BF, "a bf16 source needs the bf16 kernel");
+    constexpr unsigned SES = SB ? 2u : 4u;   // source element bytes
     constexpr int BN = 128, WGM = BM / 64, NTG = 64 * WGM * 2;   // threads per K group (the workgroup: NTG * KG)
     constexpr int PL = BF ? 1 : 2;                                 // operand planes: bf16, or f16 hi + lo
     // halo row stride HW2: TW + 2 columns, padded to a multiple of 4 where a
@@ -390,6 +404,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     constexpr int RED = (KG - 1) * WGM * 2 * 4 * 16 * 64 * 4;   // parked sums of groups 1..
     __shared__ __attribute__((aligned(16))) char lds[KG * GBYTES > RED ? KG * GBYTES : RED];
 
+    CFD_STAMP(a.stamps, 3, a.seq, 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kg = wave / (WGM * 2), wrem = wave % (WGM * 2);
@@ -410,9 +425,9 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
 
     // SGPR descriptor fields: a VGPR one costs a readfirstlane loop around every load
     const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));
-    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * SES, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
+        (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * SES : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
 
@@ -448,25 +463,32 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     const int nrounds = (max(c1 - c0, 0) + KG - 1) / KG;
     auto chunk_of = [&](int r) { return c0 + KG * r + kg; };
 
-    f4 rh[HIT];
+    typedef typename std::conditional<SB, uint2, f4>::type HT;   // one halo piece in registers
+    HT rh[HIT];
     u4 wx_h[BIT], wx_l[BIT], wy_h[BIT], wy_l[BIT];   // weight slices two steps deep
     auto load_halo = [&](int c) {
         const int cb = 32 * c;
         const bool second = cb >= a.C1;
-        const unsigned csrc4 = 4u * (second ? a.C2 : a.C1);
-        const unsigned cofs4 = 4u * ((second ? cb - a.C1 : cb) + 4 * kq);
+        const unsigned csrc = SES * (second ? a.C2 : a.C1);          // bytes per source pixel
+        const unsigned cofs = SES * ((second ? cb - a.C1 : cb) + 4 * kq);
         // one descriptor per branch (a selected descriptor would land in VGPRs)
         if (second) {
 #pragma unroll
             for (int it = 0; it < HIT; ++it) {
-                const unsigned off = hpix[it] >= 0 ? __umul24((unsigned)hpix[it], csrc4) + cofs4 : 0x80000000u;
-                rh[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs2, off, 0, 0));
+                const unsigned off = hpix[it] >= 0 ? __umul24((unsigned)hpix[it], csrc) + cofs : 0x80000000u;
+                if constexpr (SB)
+                    rh[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs2, off, 0, 0));
+                else
+                    rh[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs2, off, 0, 0));
             }
         } else {
 #pragma unroll
             for (int it = 0; it < HIT; ++it) {
-                const unsigned off = hpix[it] >= 0 ? __umul24((unsigned)hpix[it], csrc4) + cofs4 : 0x80000000u;
-                rh[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs1, off, 0, 0));
+                const unsigned off = hpix[it] >= 0 ? __umul24((unsigned)hpix[it], csrc) + cofs : 0x80000000u;
+                if constexpr (SB)
+                    rh[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs1, off, 0, 0));
+                else
+                    rh[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs1, off, 0, 0));
             }
         }
     };
@@ -476,7 +498,9 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
             const int e = gt + it * NTG;
             if (e < NPX * 8) {
                 const int off = xswz(e >> 3, kq >> 1) + (kq & 1) * 8;
-                if constexpr (BF) {
+                if constexpr (SB) {   // already bf16: the 8 loaded bytes as they are
+                    *(uint2*)(halo + off) = rh[it];
+                } else if constexpr (BF) {
                     *(bf16x4*)(halo + off) = __builtin_convertvector(rh[it], bf16x4);
                 } else {
                     uint2 hv, lv;
@@ -597,12 +621,14 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
             store_halo();
         }
         __syncthreads();
+        CFD_STAMP(a.stamps, 3, a.seq, 2);
         for (int s = 0; s < nsteps; s += 2) {
             step(s, wx_h, wx_l, wy_h, wy_l);
             if (s + 1 < nsteps) step(s + 1, wy_h, wy_l, wx_h, wx_l);
         }
     }
 
+    CFD_STAMP(a.stamps, 3, a.seq, 3);
     // combine the K groups through LDS: groups 1.. park their sums, group 0 adds
     // them in group order (fixed summation order)
     if constexpr (KG > 1) {
@@ -662,6 +688,10 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
                     if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][e];
                 }
             }
+#ifdef CFD_STAMPS
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
+        CFD_STAMP(a.stamps, 3, a.seq, 4);
         return;
     }
 #pragma unroll
@@ -711,12 +741,19 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0 && !a.wlo, CFD_ESHAPE, "conv_h bf16: 3x3 stride-1 with a 16/32/64-divisible width");
         const dim3 g = grid(256, 128);
-        if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true>), g, dim3(512), 0, st, a);
-        else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, true>), g, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, true>), g, dim3(512), 0, st, a);
+        if (a.src_bf16) {
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true, true>), g, dim3(512), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, true, true>), g, dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, true, true>), g, dim3(512), 0, st, a);
+        } else {
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true>), g, dim3(512), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, true>), g, dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, true>), g, dim3(512), 0, st, a);
+        }
         check_launch("conv_h_kernel");
         return splits;
     }
+    CFD_REQUIRE(!a.src_bf16, CFD_ESTATE, "internal: a bf16 convolution source needs the K1hb kernel");
     if (variant == 20) {   // K1h: 256-pixel blocks
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0, CFD_ESHAPE, "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");

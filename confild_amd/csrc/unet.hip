@@ -291,6 +291,7 @@ struct Act {
     int Cb = 0;
     int H = 0, W = 0;
     int C() const { return Ca + Cb; }
+    bool bf16 = false;   // a holds bf16 (a GroupNorm's out_bf16 output; read by K1hb only)
 };
 
 struct Workspace {
@@ -447,7 +448,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     // nothing else, so it is not stored (the GroupNorm of in_layers' output
     // without a tape)
     auto gn = [&](const Act& in, const std::string& pre, int silu, float** ss, float** stats,
-                  bool keep_raw = true) -> Act {
+                  bool keep_raw = true, bool bf16_out = false) -> Act {
         cfd::GnArgs g{};
         g.src1 = in.a;
         g.src2 = in.b;
@@ -482,11 +483,14 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         if (gn_log && launch)   // development: one line per GroupNorm, in launch order
             fprintf(stderr, "GN %s %dx%d C=%d+%d ksplits=%d kres=%d kx=%d silu=%d\n", pre.c_str(), in.H, in.W, g.C1,
                     g.C2, g.kpart ? g.ksplits : 0, g.kres ? 1 : 0, g.kx ? 1 : 0, silu);
+        g.out_bf16 = bf16_out ? 1 : 0;
         if (launch) cfd::launch_gn(g, B, st);
-        return Act{nbuf, in.C(), nullptr, 0, in.H, in.W};
+        Act r{nbuf, in.C(), nullptr, 0, in.H, in.W};
+        r.bf16 = bf16_out;
+        return r;
     };
-    auto conv = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up,
-                    const float* embp, const float* resp, float* out) {
+    auto conv_args = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up,
+                         const float* embp, const float* resp, float* out) {
         cfd::ConvArgs a{};
         a.src1 = in.a;
         a.src2 = in.b;
@@ -513,8 +517,26 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         a.Cout = cout;
         a.M = B * a.Hout * a.Wout;
         a.K = ks * ks * a.Ctot;
+        a.src_bf16 = in.bf16 ? 1 : 0;
+        return a;
+    };
+    // config E: a ResBlock GroupNorm writes bf16 where its consumer convolution runs
+    // on K1hb, which rounds the operand to bf16 as it stages it -- the same bits
+    // (CFD_GN_BF16OUT=0 keeps fp32 outputs)
+    static const int gn_bf16out = getenv("CFD_GN_BF16OUT") ? atoi(getenv("CFD_GN_BF16OUT")) : 1;
+    auto feeds_k1hb = [&](const Act& in, const std::string& pre, int cout) -> bool {
+        if (!gn_bf16out || h->compute != CFD_COMPUTE_BF16) return false;
+        Act n{nbuf, in.C(), nullptr, 0, in.H, in.W};
+        const cfd::ConvArgs a = conv_args(n, pre, cout, 3, 1, 0, nullptr, nullptr, nullptr);
+        return a.wbf && !a.wlo && cfd::conv_runs_k1hb(a, plan_checked(a, kSplitCap));
+    };
+    auto conv = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up,
+                    const float* embp, const float* resp, float* out) {
+        const cfd::ConvArgs a = conv_args(in, pre, cout, ks, stride, up, embp, resp, out);
         flush();
         const cfd::ConvPlan plan = plan_checked(a, kSplitCap);
+        CFD_REQUIRE(!a.src_bf16 || cfd::conv_runs_k1hb(a, plan), CFD_ESTATE,
+                    "internal: bf16 GroupNorm output feeds a convolution other than K1hb at " + pre);
         static const int conv_log = getenv("CFD_CONV_LOG") ? atoi(getenv("CFD_CONV_LOG")) : 0;
         if (conv_log && launch)   // development: one line per convolution, in launch order
             fprintf(stderr, "CONV %s %dx%d C=%d+%d->%d ks=%d s=%d up=%d M=%d kx=%d bm=%d bn=%d nw=%d splits=%d\n",
@@ -589,7 +611,8 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 pending_skip = -1;
                 const size_t nout = (size_t)B * cur.H * cur.W * r.cout;
                 // h = in_layers(x) + emb_layers(emb)   (unet.py:236-254)
-                const Act xin = gn(cur, r.pre + ".in_layers.0", 1, &rec.ss1, &rec.st1);
+                const Act xin = gn(cur, r.pre + ".in_layers.0", 1, &rec.ss1, &rec.st1, true,
+                                   feeds_k1hb(cur, r.pre + ".in_layers.2", r.cout));
                 // skip(x) first (its split-K reduction is flushed by the next
                 // convolution), so that in_layers' deferred reduction meets the
                 // out_layers GroupNorm directly   (unet.py:255-256)
@@ -605,7 +628,8 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, hb);
                 rec.h1 = hb;
                 const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
-                const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2, /*keep_raw=*/tape != nullptr);
+                const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2, /*keep_raw=*/tape != nullptr,
+                                  feeds_k1hb(th, r.pre + ".out_layers.3", r.cout));
                 float* out = dest(cur.a, cur.b, nout);
                 conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};

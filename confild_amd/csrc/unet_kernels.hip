@@ -137,6 +137,16 @@ __global__ __launch_bounds__(1024) void gn_finalize_kernel(GnArgs a) {
     }
 }
 
+// store 4 consecutive channels of a GroupNorm output at element offset e of a.out:
+// fp32, or (a.out_bf16) bf16 by the same RNE conversion K1hb applies when it
+// stages an fp32 operand (v_cvt_pk_bf16_f32), so the consumer sees the same bits
+__device__ __forceinline__ void gn_store4(const GnArgs& a, int64_t e, const f4& y) {
+    if (a.out_bf16)
+        *(bf16x4*)((__bf16*)(void*)a.out + e) = __builtin_convertvector(y, bf16x4);
+    else
+        *(f4*)(a.out + e) = y;
+}
+
 // y = x*scale + shift (+ SiLU), one float4 per thread, written as one
 // contiguous (B, HW, Ctot) tensor (the concat of two sources materialised here).
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
@@ -157,7 +167,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
     }
-    *(f4*)(a.out + pix * a.Ctot + c0) = v;
+    gn_store4(a, pix * a.Ctot + c0, v);
 }
 
 // K3f: the same GroupNorm(+SiLU) in ONE launch: workgroup = (sample, group).
@@ -231,7 +241,7 @@ __global__ __launch_bounds__(256) void gn_fused_kernel(GnArgs a) {
         sc[j] = sh[0][4 * q + j];
         sf[j] = sh[1][4 * q + j];
     }
-    float* dst = a.out + b * HW * Ctot + c;
+    const int64_t dst = b * HW * Ctot + c;
     for (int p = r0; p < HW; p += rows) {
         f4 v = *(const f4*)(src + (int64_t)p * ld);
 #pragma unroll
@@ -239,7 +249,7 @@ __global__ __launch_bounds__(256) void gn_fused_kernel(GnArgs a) {
             v[j] = v[j] * sc[j] + sf[j];
             if (a.silu) v[j] = silu_f(v[j]);
         }
-        *(f4*)(dst + (int64_t)p * Ctot) = v;
+        gn_store4(a, dst + (int64_t)p * Ctot, v);
     }
 }
 
@@ -257,6 +267,7 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     const int rows = NT / nq;
     CFD_DASSERT(grp < 32 && nq >= 1 && (HW + rows - 1) / rows <= IPT);   // every pixel has a register slot
     const int t = threadIdx.x;
+    CFD_STAMP(a.stamps, 4, a.seq, 0);
     const bool act = t < rows * nq;
     const int q = t % nq, r0 = t / nq;
     const int c = grp * cpg + 4 * q;
@@ -283,42 +294,38 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
         const float* __restrict__ kres = a.kres;
         float* __restrict__ kx = a.kx;
         const int64_t ib = (b * HW + r0) * a.C1 + c, istep = (int64_t)rows * a.C1;
+        // the residual, slab 0 and the first UN slabs are one round of loads in
+        // flight (the split-K levels are latency-bound: every dependent round is a
+        // memory latency); the slabs are added in split order, as splitk_reduce does
+        f4 rs[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int p = r0 + k * rows;
+            rs[k] = kres && act && p < HW ? *(const f4*)(kres + ib + k * istep) : f4{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const int p = r0 + k * rows;
             v[k] = act && p < HW ? *(const f4*)(kpart + ib + k * istep) : f4{0.f, 0.f, 0.f, 0.f};
         }
-        // UN slabs' loads in flight per round (one slab per round waited one
-        // memory latency per split: 16 at the 8^2 level), added in split order
-        constexpr int UN = IPT <= 2 ? 4 : IPT <= 4 ? 2 : 1;
-        int sp = 1;
-        for (; sp + UN - 1 < a.ksplits; sp += UN) {
+        constexpr int UN = IPT <= 2 ? 8 : IPT <= 4 ? 4 : 1;
+        for (int sp = 1; sp < a.ksplits; sp += UN) {
             f4 u[UN][IPT];
 #pragma unroll
             for (int q2 = 0; q2 < UN; ++q2)
 #pragma unroll
                 for (int k = 0; k < IPT; ++k) {
                     const int p = r0 + k * rows;
-                    u[q2][k] = act && p < HW ? *(const f4*)(kpart + (sp + q2) * slab + ib + k * istep)
-                                             : f4{0.f, 0.f, 0.f, 0.f};
+                    u[q2][k] = sp + q2 < a.ksplits && act && p < HW
+                                   ? *(const f4*)(kpart + (sp + q2) * slab + ib + k * istep)
+                                   : f4{0.f, 0.f, 0.f, 0.f};
                 }
 #pragma unroll
             for (int q2 = 0; q2 < UN; ++q2)
+                if (sp + q2 < a.ksplits) {
 #pragma unroll
-                for (int k = 0; k < IPT; ++k) v[k] += u[q2][k];
-        }
-        for (; sp < a.ksplits; ++sp) {
-#pragma unroll
-            for (int k = 0; k < IPT; ++k) {
-                const int p = r0 + k * rows;
-                if (act && p < HW) v[k] += *(const f4*)(kpart + sp * slab + ib + k * istep);
-            }
-        }
-        f4 rs[IPT];
-#pragma unroll
-        for (int k = 0; k < IPT; ++k) {
-            const int p = r0 + k * rows;
-            rs[k] = kres && act && p < HW ? *(const f4*)(kres + ib + k * istep) : f4{0.f, 0.f, 0.f, 0.f};
+                    for (int k = 0; k < IPT; ++k) v[k] += u[q2][k];
+                }
         }
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
@@ -341,6 +348,7 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
             v[k] = act && p < HW ? *(const f4*)(src + (int64_t)p * ld) : f4{0.f, 0.f, 0.f, 0.f};
         }
     }
+    CFD_STAMP(a.stamps, 4, a.seq, 1);
     double s = 0, s2 = 0;
 #pragma unroll
     for (int k = 0; k < IPT; ++k)
@@ -377,6 +385,7 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
         }
     }
     __syncthreads();
+    CFD_STAMP(a.stamps, 4, a.seq, 2);
     if (!act) return;
     f4 sc, sf;
 #pragma unroll
@@ -384,7 +393,7 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
         sc[j] = sh[0][4 * q + j];
         sf[j] = sh[1][4 * q + j];
     }
-    float* dst = a.out + b * HW * Ctot + c;
+    const int64_t dst = b * HW * Ctot + c;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const int p = r0 + k * rows;
@@ -395,9 +404,13 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
                 y[j] = v[k][j] * sc[j] + sf[j];
                 if (a.silu) y[j] = silu_f(y[j]);
             }
-            *(f4*)(dst + (int64_t)p * Ctot) = y;
+            gn_store4(a, dst + (int64_t)p * Ctot, y);
         }
     }
+#ifdef CFD_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    CFD_STAMP(a.stamps, 4, a.seq, 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -455,7 +468,10 @@ __device__ __forceinline__ void split4_mix(const f4& x, uint2& hi, uint2& lo) {
 // (tests/test_gpu_unet_split.py).  hi and lo tiles use the bf16 LDS layout.
 // NW waves as (NW/2) x 2; 8 waves with BM = 128 halve the weight-tile reads per
 // output pixel at the same per-wave tile.
-template <int BM, int BN, bool TMODE, int MODE, int NW = 4, bool BUFA = false>
+// PF: K tiles in flight through registers (1: the next tile, the double buffer;
+// 2-3: a register ring for the short, latency-bound K chains at small batch --
+// the same tiles in the same order, so the same sums)
+template <int BM, int BN, bool TMODE, int MODE, int NW = 4, bool BUFA = false, int PF = 1>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(ConvArgs a) {
     constexpr bool BF = MODE == 1, SP = MODE == 2;
     constexpr int BK = 32;
@@ -477,6 +493,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     // index arithmetic that made the kernel VALU-issue-bound
     __shared__ int pixtab[BUFA ? 9 * BM : 1];
 
+    CFD_STAMP(a.stamps, 1, a.seq, 0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     // XCD-contiguous tile order (a.xcd): workgroup L runs on XCD L % 8 (round-robin
@@ -554,8 +571,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     };
 
     const int smask = a.stride - 1, sshift = a.stride >> 1;
-    f4 ra[AIT], rb[BIT];
-    uint2 rbh[BIT], rbl[BIT];
+    f4 ra[PF][AIT], rb[PF][BIT];
+    uint2 rbh[PF][BIT], rbl[PF][BIT];
     // buffer-addressed path: resources, per-row weight offsets, the pixel table
     constexpr int WES = (BF || SP) ? 2 : 4;   // weight element bytes
     const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR descriptor fields
@@ -608,8 +625,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             pixtab[e] = pix;
         }
         __syncthreads();
+        CFD_STAMP(a.stamps, 1, a.seq, 1);
     }
-    auto load_tile = [&](int kt) {
+    auto load_tile = [&](int kt, int sl) {
         int cb, dy, dx;
         kpos_of(kt, cb, dy, dx);
         const int c0 = cb + 4 * kq;
@@ -624,17 +642,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             for (int it = 0; it < AIT; ++it) {
                 const int pix = pixtab[tap * BM + rsub + it * RPP];
                 const unsigned off = pix >= 0 ? __umul24((unsigned)pix, csrc4) + cofs4 : 0x80000000u;
-                ra[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
+                ra[sl][it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
             }
             const int soff = kpos * WES;
 #pragma unroll
             for (int it = 0; it < BIT; ++it) {
                 if constexpr (BF || SP)
-                    rbh[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, b_voff[it], soff, 0));
+                    rbh[sl][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, b_voff[it], soff, 0));
                 if constexpr (SP)
-                    rbl[it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, b_voff[it], soff, 0));
+                    rbl[sl][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, b_voff[it], soff, 0));
                 if constexpr (!BF && !SP)
-                    rb[it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rwh, b_voff[it], soff, 0));
+                    rb[sl][it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rwh, b_voff[it], soff, 0));
             }
         } else {
 #pragma unroll
@@ -665,27 +683,27 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                 v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0)
                               : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
             }
-            ra[it] = v;
+            ra[sl][it] = v;
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
             if constexpr (BF || SP)
-                rbh[it] = b_ok[it] ? *(const uint2*)(wrow_bf[it] + kpos) : uint2{0u, 0u};
+                rbh[sl][it] = b_ok[it] ? *(const uint2*)(wrow_bf[it] + kpos) : uint2{0u, 0u};
             if constexpr (SP)
-                rbl[it] = b_ok[it] ? *(const uint2*)(wrow_lo[it] + kpos) : uint2{0u, 0u};
+                rbl[sl][it] = b_ok[it] ? *(const uint2*)(wrow_lo[it] + kpos) : uint2{0u, 0u};
             if constexpr (!BF && !SP)
-                rb[it] = b_ok[it] ? *(const f4*)(wrow[it] + kpos) : f4{0.f, 0.f, 0.f, 0.f};
+                rb[sl][it] = b_ok[it] ? *(const f4*)(wrow[it] + kpos) : f4{0.f, 0.f, 0.f, 0.f};
         }
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf, int sl) {
         if constexpr (SP) {
             // hi tile at [0, BM*BK/2) floats, lo tile after it (same bf16 layout)
 #pragma unroll
             for (int it = 0; it < AIT; ++it) {
                 // hi = f16(x) (RNE, packed convert), lo = f16(x - hi) in one v_fma_mix per value
                 uint2 hv, lv;
-                split4_mix(ra[it], hv, lv);
+                split4_mix(ra[sl][it], hv, lv);
                 const int off = lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8;
                 *(uint2*)((char*)As[buf] + off) = hv;
                 *(uint2*)((char*)As[buf] + BM * BK * 2 + off) = lv;
@@ -693,24 +711,24 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
 #pragma unroll
             for (int it = 0; it < BIT; ++it) {
                 const int off = lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8;
-                *(uint2*)((char*)Bs[buf] + off) = rbh[it];
-                *(uint2*)((char*)Bs[buf] + BN * BK * 2 + off) = rbl[it];
+                *(uint2*)((char*)Bs[buf] + off) = rbh[sl][it];
+                *(uint2*)((char*)Bs[buf] + BN * BK * 2 + off) = rbl[sl][it];
             }
         } else if constexpr (BF) {
             // thread kq holds k = 4kq..4kq+3: chunk kq/2, half kq%2
 #pragma unroll
             for (int it = 0; it < AIT; ++it) {
-                const bf16x4 v = __builtin_convertvector(ra[it], bf16x4);
+                const bf16x4 v = __builtin_convertvector(ra[sl][it], bf16x4);
                 *(bf16x4*)((char*)As[buf] + lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8) = v;
             }
 #pragma unroll
             for (int it = 0; it < BIT; ++it)
-                *(uint2*)((char*)Bs[buf] + lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8) = rbh[it];
+                *(uint2*)((char*)Bs[buf] + lds_swz_bf(rsub + it * RPP, kq >> 1) + (kq & 1) * 8) = rbh[sl][it];
         } else {
 #pragma unroll
-            for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][lds_swz(rsub + it * RPP, kq)]) = ra[it];
+            for (int it = 0; it < AIT; ++it) *(f4*)(&As[buf][lds_swz(rsub + it * RPP, kq)]) = ra[sl][it];
 #pragma unroll
-            for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][lds_swz(rsub + it * RPP, kq)]) = rb[it];
+            for (int it = 0; it < BIT; ++it) *(f4*)(&Bs[buf][lds_swz(rsub + it * RPP, kq)]) = rb[sl][it];
         }
     };
 
@@ -721,13 +739,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
         for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
     const int g2 = 2 * (lane >> 4), li = lane & 15;
-    if (kt0 < kt1) {
-        load_tile(kt0);
-        store_tile(0);
-        __syncthreads();
-        for (int kt = kt0; kt < kt1; ++kt) {
-            const int cur = (kt - kt0) & 1;
-            if (kt + 1 < kt1) load_tile(kt + 1);
+    auto compute = [&](int cur) {
             if constexpr (SP) {
                 const int g = lane >> 4;
                 h8v fah[TM], fal[TM], fbh[TN], fbl[TN];
@@ -781,10 +793,38 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                         for (int j = 0; j < TN; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
             }
-            if (kt + 1 < kt1) store_tile(cur ^ 1);
+    };
+    if (kt0 < kt1) {
+        load_tile(kt0, 0);
+#pragma unroll
+        for (int p = 1; p < PF; ++p) load_tile(min(kt0 + p, kt1 - 1), p);
+        store_tile(0, 0);
+        __syncthreads();
+        CFD_STAMP(a.stamps, 1, a.seq, 2);
+        // step kt: tile kt + PF into the register slot tile kt left (clamped: a
+        // repeated last tile keeps every load unconditional, so the wait before a
+        // store is a counted vmcnt), MFMAs on LDS stage cur, then tile kt + 1 from
+        // its slot into the other stage
+        auto step = [&](int kt, int j) {
+            const int cur = (kt - kt0) & 1;
+            if constexpr (PF == 1) {
+                if (kt + 1 < kt1) load_tile(kt + 1, 0);
+            } else {
+                load_tile(min(kt + PF, kt1 - 1), j);
+            }
+            compute(cur);
+            if (kt + 1 < kt1) store_tile(cur ^ 1, (j + 1) % PF);
             __syncthreads();
+        };
+        for (int kt = kt0; kt < kt1; kt += PF) {
+            step(kt, 0);
+            if constexpr (PF > 1)
+                if (kt + 1 < kt1) step(kt + 1, 1);
+            if constexpr (PF > 2)
+                if (kt + 2 < kt1) step(kt + 2, 2);
         }
     }
+    CFD_STAMP(a.stamps, 1, a.seq, 3);
 
     const int g4 = 4 * (lane >> 4);
     if constexpr (SP) {  // undo the power-of-two weight scale (exact)
@@ -831,6 +871,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                 if (a.res) val = *(const f4*)(a.res + o) + val;
                 *(f4*)(a.out + o) = val;
             }
+#ifdef CFD_STAMPS
+            __builtin_amdgcn_s_waitcnt(0);
+#endif
+            CFD_STAMP(a.stamps, 1, a.seq, 4);
             return;
         }
     }
@@ -848,6 +892,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                     if (n < a.Cout) part[(int64_t)m * a.Cout + n] = acc[i][j][r];
                 }
             }
+        CFD_STAMP(a.stamps, 1, a.seq, 4);
         return;
     }
     // epilogue: (acc + bias) (+ emb[b, n]); residual + h
@@ -869,6 +914,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             }
         }
     }
+    CFD_STAMP(a.stamps, 1, a.seq, 4);
 }
 
 // sum of split-K partials in split order + the conv epilogue
@@ -878,17 +924,20 @@ __global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
     if (i4 >= total4) return;
     const int64_t i = i4 * 4;
     const int64_t slab = (int64_t)a.M * a.Cout;
+    // the residual, slab 0 and up to 15 more slabs in one round of loads (each
+    // dependent round is a memory latency), added in split order
+    const f4 rv = a.res ? *(const f4*)(a.res + i) : f4{0.f, 0.f, 0.f, 0.f};
     f4 s = *(const f4*)(a.part + i);
-    int k = 1;
-    for (; k + 3 < splits; k += 4) {   // four slabs' loads in flight, added in split order
-        const f4 u0 = *(const f4*)(a.part + k * slab + i), u1 = *(const f4*)(a.part + (k + 1) * slab + i);
-        const f4 u2 = *(const f4*)(a.part + (k + 2) * slab + i), u3 = *(const f4*)(a.part + (k + 3) * slab + i);
-        s += u0;
-        s += u1;
-        s += u2;
-        s += u3;
+    constexpr int UN = 15;
+    for (int k = 1; k < splits; k += UN) {
+        f4 u[UN];
+#pragma unroll
+        for (int q = 0; q < UN; ++q)
+            u[q] = k + q < splits ? *(const f4*)(a.part + (k + q) * slab + i) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < UN; ++q)
+            if (k + q < splits) s += u[q];
     }
-    for (; k < splits; ++k) s += *(const f4*)(a.part + k * slab + i);
     const int64_t m = i / a.Cout;
     const int n = (int)(i - m * a.Cout);
     const int bb = (int)(m / (a.Hout * a.Wout));
@@ -897,7 +946,7 @@ __global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
     for (int j = 0; j < 4; ++j) {
         float y = a.bias ? s[j] + a.bias[n + j] : s[j];
         if (a.emb) y = y + a.emb[(int64_t)bb * a.emb_stride + n + j];
-        if (a.res) y = a.res[i + j] + y;
+        if (a.res) y = rv[j] + y;
         v[j] = y;
     }
     *(f4*)(a.out + i) = v;
@@ -1568,6 +1617,11 @@ int gn_chunks(int HW) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(kGnMaxChunks, std::max<int64_t>(HW / 64, small)));
 }
 
+static unsigned long long* g_stamps = nullptr;
+void stamps_set(unsigned long long* buf) { g_stamps = buf; }
+unsigned long long* stamps_buf() { return g_stamps; }
+static int g_seq = 0;   // launch sequence number of the U-Net kernels (timestamps)
+
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -1588,6 +1642,8 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     GnArgs a = a0;
     a.nchunks = gn_chunks(a.HW);
     a.B = B;
+    a.stamps = g_stamps;
+    a.seq = g_seq++;
     CFD_REQUIRE(!a.kpart || gn_takes_splitk(a, B), CFD_ESTATE, "internal: split-K source on a GroupNorm path without it");
     static const int fused = env_int("CFD_GN_FUSED", 1);
     static const int big = env_int("CFD_GN_BIG", 1);   // 0: the one-launch kernels at every size
@@ -1743,6 +1799,16 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
 
 template <bool TMODE, int MODE, bool BUFA>
 static void launch_conv_tiles_(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
+    if constexpr (!TMODE && MODE == 2 && BUFA) {   // the split-f16 forward: register-ring depths
+        if (p.nw == 8 && p.bm == 128 && p.bn == 128 && p.pf == 2) {
+            hipLaunchKernelGGL((conv_gemm_kernel<128, 128, false, 2, 8, true, 2>), grid, dim3(512), 0, st, a);
+            return;
+        }
+        if (p.nw == 8 && p.bm == 128 && p.bn == 128 && p.pf == 3) {
+            hipLaunchKernelGGL((conv_gemm_kernel<128, 128, false, 2, 8, true, 3>), grid, dim3(512), 0, st, a);
+            return;
+        }
+    }
     if (p.nw == 8 && p.bm == 128 && p.bn == 128)
         hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE, 8, BUFA>), grid, dim3(512), 0, st, a);
     else if (p.bm == 128 && p.bn == 128)
@@ -1767,19 +1833,28 @@ void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st) {
     check_launch("splitk_reduce_kernel");
 }
 
+// K1x / K1h need 32-bit operand offsets at the real batch; else K1s 128x128 tiles of 8
+// waves with the same splits (CFD_CONV_FORCE_K1S=1 forces that fallback: tests)
+static bool conv_x_falls_back(const ConvArgs& a) {
+    static const int force_k1s = env_int("CFD_CONV_FORCE_K1S", 0);
+    const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
+    return force_k1s || !(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31));
+}
+
+bool conv_runs_k1hb(const ConvArgs& a, const ConvPlan& p) { return p.kx == 22 && !conv_x_falls_back(a); }
+
 int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defer) {
     ConvPlan p = p0;
-    // K1x / K1h need 32-bit operand offsets at the real batch; else K1s 128x128 tiles of 8
-    // waves with the same splits (CFD_CONV_FORCE_K1S=1 forces that fallback: tests)
-    static const int force_k1s = env_int("CFD_CONV_FORCE_K1S", 0);
-    if (p.kx >= 0) {
-        const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
-        if (force_k1s || !(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31))) {
-            p.kx = -1;
-            p.bm = p.bn = 128;
-            p.nw = 8;
-        }
+    if (p.kx >= 0 && conv_x_falls_back(a)) {
+        p.kx = -1;
+        p.bm = p.bn = 128;
+        p.nw = 8;
     }
+    CFD_REQUIRE(!a.src_bf16 || p.kx == 22, CFD_ESTATE, "internal: a bf16 convolution source needs the K1hb kernel");
+    // K1s register-ring depth (development: CFD_CONV_PF; the tiles and their order,
+    // hence the sums, do not depend on it)
+    static const int pf = env_int("CFD_CONV_PF", 1);
+    if (p.kx < 0) p.pf = pf >= 1 && pf <= 3 ? pf : 1;
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
     CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot, CFD_ESHAPE, "conv K mismatch");
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
@@ -1791,6 +1866,8 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     static const int bufaddr = env_int("CFD_CONV_BUFADDR", 1);
     static const int ldsepi = env_int("CFD_CONV_LDSEPI", 1);
     ConvArgs b = a;
+    b.stamps = g_stamps;
+    b.seq = g_seq++;
     // float4 rows need Cout % 4 == 0 and 16-B aligned bias / emb / res / out rows
     b.ldsepi = ldsepi && a.Cout % 4 == 0 && a.emb_stride % 4 == 0;
     // 1: splits-fastest XCD order; 2: m-fastest (weight-sharing) order; 3: order 2 where
@@ -1925,3 +2002,16 @@ void launch_linear(const float* x, const float* W, const float* bias, float* y, 
 }
 
 }  // namespace cfd
+
+// development hook of the CFD_STAMPS build (not in include/confild.h): the
+// buffer the instrumented kernels append their timestamps to (null: off)
+extern "C" int cfd_stamps_set(void* buf) {
+#ifdef CFD_STAMPS
+    cfd::stamps_set((unsigned long long*)buf);
+    return CFD_OK;
+#else
+    (void)buf;
+    cfd::set_error("cfd_stamps_set: not a CFD_STAMPS build (make STAMPS=1)");
+    return CFD_ESTATE;
+#endif
+}

@@ -29,6 +29,12 @@ struct GnArgs {
     const float* kres;
     float* kx;           // where the reduced sum is stored (null: nowhere, nobody reads it)
     int ksplits, kemb_stride;
+    unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
+    int seq;                      // launch sequence number (timestamps)
+    // out holds bf16 (RNE of the fp32 result, (B, HW, Ctot) of 2-byte elements):
+    // config E, where the consumer is a K1hb convolution that rounds its operand
+    // to bf16 anyway -- the same bits, half the bytes written and re-read
+    int out_bf16;
 };
 
 struct ConvArgs {
@@ -55,7 +61,13 @@ struct ConvArgs {
     int bufaddr;         // 32-bit buffer addressing of the operands (set by launch_conv where it fits)
     int ldsepi;          // K1s: epilogue through LDS, float4 rows (set by launch_conv; CFD_CONV_LDSEPI=0: off)
     int* nonfinite;      // conv_out only: set to 1 when an output is not finite (range guard), or null
+    int src_bf16;        // src1 / src2 hold bf16 (a GroupNorm's out_bf16 output): K1hb only
+    unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
+    int seq;                      // launch sequence number (timestamps)
 };
+// development: the timestamp buffer the CFD_STAMPS build's kernels write (null: off)
+void stamps_set(unsigned long long* buf);
+unsigned long long* stamps_buf();
 
 struct AttnArgs {
     const float* qkv;  // (B, T, 3C)
@@ -100,6 +112,7 @@ struct ConvPlan {
     int bm = 128, bn = 128, splits = 1;
     int nw = 4;  // waves per workgroup (8: BM = BN = 128 only)
     int kx = -1; // >= 0: run the K1x kernel variant (conv_x.hip) instead of conv_gemm_kernel
+    int pf = 1;  // K1s: K tiles in flight through registers (set by launch_conv)
 };
 
 constexpr int kGnMaxChunks = 512;
@@ -145,6 +158,9 @@ __device__ __forceinline__ void xcd_tile(int order, int& bx, int& by, int& bz) {
 // 64x64 wave tiles; variant selects the kernel and tile shape
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st);
 int conv_h_tw(const ConvArgs& a);   // K1h tile width for a shape, 0: not applicable
+// whether launch_conv runs this plan on K1hb (the bf16 halo kernel, variant 22):
+// the only convolution that reads a bf16 source (ConvArgs::src_bf16)
+bool conv_runs_k1hb(const ConvArgs& a, const ConvPlan& p);
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
 void launch_conv_out(const ConvArgs& a, hipStream_t st);
 void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t st);

@@ -98,3 +98,46 @@ def test_bf16_unet_batch_invariant(hip):
     assert torch.equal(m(x[1:3], t[1:3]), full[1:3])
     with pytest.raises(NotImplementedError):
         m.forward_tape(x, t)
+
+
+_GN_BF16_CHILD = r"""
+import json, sys, torch
+sys.path.insert(0, sys.argv[1])
+from confild_amd import synth
+from confild_amd.script_util import create_model
+out = {}
+for S, mult, B in ((16, "1,2", 3), (32, "1,2,2", 2), (64, "", 2), (128, "", 1)):
+    kw = dict(image_size=S, num_channels=128 if S >= 64 else 64, num_res_blocks=2, channel_mult=mult, num_heads=4,
+              num_head_channels=32, attention_resolutions="32,16,8" if S >= 64 else "8,4", use_bf16=True)
+    m = create_model(**kw)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in
+                       synth.unet_state_dict(9, {k: tuple(v.shape) for k, v in m.state_dict().items()}).items()})
+    m.to("cuda")
+    x = torch.from_numpy(synth.normal(3, f"gnbf/x{S}", (B, 1, S, S))).cuda()
+    t = torch.tensor([999, 400, 3][:B], dtype=torch.int64).cuda()
+    eps = m(x, t).cpu()
+    out[S] = eps.numpy().tobytes().hex()
+print(json.dumps(out))
+"""
+
+
+def test_gn_bf16_output_is_bit_identical(hip):
+    """Config E's ResBlock GroupNorms write bf16 where their consumer runs K1hb
+    (CFD_GN_BF16OUT, default on): the consumer would round the fp32 output to bf16
+    (RNE) as it stages it, so eps must be bit-identical to the fp32-output path at
+    every K1hb tile width (16^2 / 32^2 / 64^2 halo tiles) and batch, with the two
+    concatenated skip sources included (the output blocks)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for flag in ("0", "1"):
+        env = dict(os.environ, CFD_GN_BF16OUT=flag)
+        r = subprocess.run([sys.executable, "-c", _GN_BF16_CHILD, root], capture_output=True, text=True, env=env,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[flag] = json.loads(r.stdout.strip().splitlines()[-1])
+    for S in res["0"]:
+        assert res["0"][S] == res["1"][S], f"{S}^2: bf16 GroupNorm output changed eps"

@@ -1,0 +1,51 @@
+"""Launch-shape switches that must not change a single bit: they pick how the
+work is scheduled (register-ring depth of the K1s convolution tiles), never the
+tiles, their K order or the split-K boundaries, so every output's summation
+order -- and hence eps -- is unchanged.  Each setting runs in a child process
+(the switches are read once per process) over split-f16 U-Nets at the config-A
+and config-B widths, at batch 1 and 3 (the small-batch shapes the deeper rings
+are for), and the outputs are compared bit for bit with the default build."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import json, sys, torch
+sys.path.insert(0, sys.argv[1])
+from confild_amd import synth
+from confild_amd.script_util import create_model
+out = {}
+for S, mult in ((32, "1,2,3,4"), (64, "")):
+    m = create_model(image_size=S, num_channels=128, num_res_blocks=2, channel_mult=mult, num_heads=4,
+                     num_head_channels=64, attention_resolutions="32,16,8")
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in
+                       synth.unet_state_dict(11, {k: tuple(v.shape) for k, v in m.state_dict().items()}).items()})
+    m.to("cuda")
+    for B in (1, 3):
+        x = torch.from_numpy(synth.normal(4, f"knob/x{S}", (B, 1, S, S))).cuda()
+        t = torch.tensor([999, 400, 3][:B], dtype=torch.int64).cuda()
+        out[f"{S}/{B}"] = m(x, t).cpu().numpy().tobytes().hex()
+print(json.dumps(out))
+"""
+
+
+def _run(env_extra):
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([sys.executable, "-c", CHILD, ROOT], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3"])
+def test_schedule_switch_is_bit_identical(hip, knob):
+    base = _run({})
+    k, v = knob.split("=")
+    got = _run({k: v})
+    for key in base:
+        assert got[key] == base[key], f"{knob} changed eps at {key}"
