@@ -383,11 +383,14 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // GroupNorm's out_bf16 output, rounded by the same conversion): 8-byte halo
 // pieces (4 channels of 2 bytes, byte offset 2 * (pixel * C + channel)) are
 // copied to LDS as they are -- half the activation bytes, the same bits.
-template <int BM, int TW, int KG = 1, bool BF = false, bool SB = false>
-__global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
+// BN: output channels per workgroup, 128 (two wave columns) or 64 (one: at small
+// batch twice the workgroups, one wave per SIMD -- the same tiles' sums)
+template <int BM, int TW, int KG = 1, bool BF = false, bool SB = false, int BN = 128>
+__global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs a) {
     static_assert(!SB || BF, "a bf16 source needs the bf16 kernel");
     constexpr unsigned SES = SB ? 2u : 4u;   // source element bytes
-    constexpr int BN = 128, WGM = BM / 64, NTG = 64 * WGM * 2;   // threads per K group (the workgroup: NTG * KG)
+    constexpr int WGN = BN / 64, WGM = BM / 64, NTG = 64 * WGM * WGN;   // threads per K group (the workgroup: NTG * KG)
+    static_assert(BN == 64 || BN == 128, "K1h: 64 or 128 output channels per workgroup");
     constexpr int PL = BF ? 1 : 2;                                 // operand planes: bf16, or f16 hi + lo
     // halo row stride HW2: TW + 2 columns, padded to a multiple of 4 where a
     // 32-pixel fragment block spans two tile rows (TW = 16), so the second row's
@@ -401,14 +404,14 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
     constexpr int BIT = BN * 4 / NTG;                 // 16-B weight pieces per thread and plane
     constexpr int GBYTES = PL * HPLANE + 2 * BSTAGE;  // one group's halo + weight ring
     static_assert(BM % TW == 0 && BIT >= 1, "tile");
-    constexpr int RED = (KG - 1) * WGM * 2 * 4 * 16 * 64 * 4;   // parked sums of groups 1..
+    constexpr int RED = (KG - 1) * WGM * WGN * 4 * 16 * 64 * 4;   // parked sums of groups 1..
     __shared__ __attribute__((aligned(16))) char lds[KG * GBYTES > RED ? KG * GBYTES : RED];
 
     CFD_STAMP(a.stamps, 3, a.seq, 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int kg = wave / (WGM * 2), wrem = wave % (WGM * 2);
-    const int wm = wrem >> 1, wn = wrem & 1;
+    const int kg = wave / (WGM * WGN), wrem = wave % (WGM * WGN);
+    const int wm = wrem / WGN, wn = wrem % WGN;
     const int gt = tid - kg * NTG;   // thread index within the group
     char* const halo = lds + kg * GBYTES;
     char* const ring = halo + PL * HPLANE;
@@ -636,7 +639,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
         constexpr int PER_WAVE = 4 * 16 * 64;
         __syncthreads();            // the stages are free
         if (kg > 0) {
-            float* dst = red + ((kg - 1) * WGM * 2 + wrem) * PER_WAVE;
+            float* dst = red + ((kg - 1) * WGM * WGN + wrem) * PER_WAVE;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -650,7 +653,7 @@ __global__ __launch_bounds__(BM * 2 * KG, 1) void conv_h_kernel(ConvArgs a) {
         if (kg > 0) return;
 #pragma unroll
         for (int g = 1; g < KG; ++g) {
-            const float* src = red + ((g - 1) * WGM * 2 + wrem) * PER_WAVE;
+            const float* src = red + ((g - 1) * WGM * WGN + wrem) * PER_WAVE;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -757,7 +760,20 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
     if (variant == 20) {   // K1h: 256-pixel blocks
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0, CFD_ESHAPE, "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");
+        // small batch: where the 128-channel grid leaves most CUs idle (< 128
+        // workgroups of 8 waves, two per SIMD), 64-channel workgroups of 4 waves --
+        // twice the workgroups, one wave per SIMD, the same tiles' sums
+        // (CFD_CONV_SMALLN=0 keeps 128)
+        static const int smalln = getenv("CFD_CONV_SMALLN") ? atoi(getenv("CFD_CONV_SMALLN")) : 1;
         const dim3 g = grid(256, 128);
+        if (smalln && (int64_t)g.x * g.y * g.z < 128 && a.Cout % 64 == 0) {
+            const dim3 g64 = grid(256, 64);
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, false, false, 64>), g64, dim3(256), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, false, false, 64>), g64, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, false, false, 64>), g64, dim3(256), 0, st, a);
+            check_launch("conv_h_kernel");
+            return splits;
+        }
         if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
         else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
         else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);

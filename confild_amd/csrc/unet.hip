@@ -737,6 +737,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     // parameter-gradient scratch (pg_ws: sized in the dry walk of cfd_unet_param_grad_workspace_bytes)
     float *wpart = nullptr, *cpart = nullptr, *crow = nullptr, *demb = nullptr, *dth1 = nullptr, *gpp = nullptr;
     float* wact = nullptr;
+    unsigned* wamax = nullptr;
     size_t wcap = 0, ccap = 0;
     if (pg_ws) {
         int cmax = 0;
@@ -750,6 +751,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         demb = ws.take((size_t)B * h->tdim);
         dth1 = ws.take((size_t)B * h->tdim);
         gpp = ws.take((size_t)B * cfd::kGnMaxChunks * 2 * cmax * 2);
+        wamax = (unsigned*)ws.take(64);   // the split weight gradient's operand ranges
     }
     if (ws.dry) return;
     std::vector<size_t> goff;
@@ -783,6 +785,9 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         a.ss = ss;
         a.silu = silu;
         a.part = wpart;
+        // split-f16 weight-gradient products in split compute (the exact fp32-MFMA
+        // kernel in the fp32 / bf16 modes)
+        a.amax_out = h->compute == CFD_COMPUTE_SPLIT_F16 ? wamax : nullptr;
         a.P = (int64_t)B * Hout * Wout;
         a.Cout = cout;
         a.Hin = X.H;

@@ -1799,7 +1799,18 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
 
 template <bool TMODE, int MODE, bool BUFA>
 static void launch_conv_tiles_(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-    if constexpr (!TMODE && MODE == 2 && BUFA) {   // the split-f16 forward: register-ring depths
+    if constexpr (!TMODE && MODE == 2 && BUFA) {   // the split-f16 forward
+        // small batch: where the 128 x 128 grid leaves most CUs idle (< 128
+        // workgroups of 8 waves, two per SIMD), 128 x 64 tiles of 8 waves (32 x 32
+        // each) -- twice the workgroups, half the work per wave, the same tiles'
+        // sums (CFD_CONV_SMALLN=0 keeps 128 x 128)
+        static const int smalln = env_int("CFD_CONV_SMALLN", 1);
+        if (smalln && p.nw == 8 && p.bm == 128 && p.bn == 128 && (int64_t)grid.x * grid.y * grid.z < 128 &&
+            a.Cout % 64 == 0) {
+            const dim3 g64(grid.x, (unsigned)ceil_div(a.Cout, 64), grid.z);
+            hipLaunchKernelGGL((conv_gemm_kernel<128, 64, false, 2, 8, true>), g64, dim3(512), 0, st, a);
+            return;
+        }
         if (p.nw == 8 && p.bm == 128 && p.bn == 128 && p.pf == 2) {
             hipLaunchKernelGGL((conv_gemm_kernel<128, 128, false, 2, 8, true, 2>), grid, dim3(512), 0, st, a);
             return;
@@ -1953,11 +1964,13 @@ void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* 
                        kf, vf);
     check_launch("attn_kv_split_kernel");
     // K4d (default; CFD_ATTN_DMA=0 restores K4s): fragments staged per workgroup
-    // by LDS-DMA, 8 waves (128 queries) per workgroup where T >= 512, else 4 (the
-    // choice changes no result: every query's arithmetic is the same)
+    // by LDS-DMA, 8 waves (128 queries) per workgroup where T >= 512 and that still
+    // gives >= 256 workgroups, else 4 -- at batch 1 the 64-query workgroups double
+    // the parallelism of the 32^2 blocks (the choice changes no result: every
+    // query's arithmetic is the same)
     static const int dma = env_int("CFD_ATTN_DMA", 1);
     if (dma) {
-        const int w8 = a.T >= 512;
+        const int w8 = a.T >= 512 && (int64_t)B * heads * ceil_div(a.T, 128) >= 256;
         const dim3 grid((unsigned)ceil_div(a.T, w8 ? 128 : 64), heads, B);
         const dim3 blk(w8 ? 512 : 256);
         switch (CH * 2 + w8) {

@@ -220,24 +220,213 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(WgradArgs a, const f
         }
 }
 
+// ---------------------------------------------------------------------------
+// Split-f16 weight gradient (default where the 128-tile kernel applies): the same
+// product dW[m][n] = sum over pixels k of dY[k][m] * X[k][n], on f16 matrix cores
+// at fp32-level accuracy, as the forward convolutions run it:
+// both operands are scaled by a power of two into the f16 range -- s_y from
+// max|dY| and s_x from max|X| over the whole tensors (absmax_kernel, atomicMax of
+// non-negative float bits: exact and order-free) -- and split x = hi + lo (hi =
+// f16(x), lo = f16(x - hi), RNE); each product runs as lo.hi + hi.lo + hi.hi on
+// v_mfma_f32_16x16x32_f16 with fp32 accumulation, and the sums are multiplied
+// back by 1 / (s_x s_y) (exact).  Operands below 2^-14 of their tensor's maximum
+// keep fewer bits in their halves, but their absolute error stays at the 2^-25
+// level of the largest product they are summed with.
+// Tiles: 128 output rows (Cout) x 128 columns (one tap's channels) per block, 4
+// waves of 64 x 64; pixels in steps of 32 (one MFMA depth).  The operands are
+// staged transposed, [row][pixel] f16 rows of 64 B (a thread: 4 rows x 4 pixels),
+// in the K1s fragment layout; the next step's loads are in flight during the
+// MFMAs.  Partial slabs and wgrad_accum_kernel as in the fp32 kernel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wg_swz(int row, int chunk) {   // unet_kernels.hip lds_swz_bf
+    return row * 64 + ((chunk + 2 * ((row >> 2) & 1)) & 3) * 16;
+}
+// hi = f16(s x), lo = f16(s x - hi) of 4 values, packed as 2 x (2 halfs)
+__device__ __forceinline__ void wg_split4(f4 x, float s, uint2& hi, uint2& lo) {
+    typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+    typedef float f2_ __attribute__((ext_vector_type(2)));
+    x *= s;
+    hi.x = __builtin_bit_cast(unsigned, __builtin_convertvector((f2_){x[0], x[1]}, h2_));
+    hi.y = __builtin_bit_cast(unsigned, __builtin_convertvector((f2_){x[2], x[3]}, h2_));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.x) : "v"(x[0]), "v"(hi.x));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.x) : "v"(x[1]), "v"(hi.x));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.y) : "v"(x[2]), "v"(hi.y));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.y) : "v"(x[3]), "v"(hi.y));
+}
+// power of two s with max * s in [0.5, 1) (1 for an all-zero tensor)
+__device__ __forceinline__ float wg_scale(unsigned amax_bits) {
+    const float m = __uint_as_float(amax_bits);
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+    int e;
+    (void)frexpf(m, &e);
+    return ldexpf(1.f, -e);
+}
+
+// max |x| over n floats (n % 4 == 0) into *out (atomicMax of the float bits)
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t n4, unsigned* out) {
+    float m = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const f4 v = *(const f4*)(x + 4 * i);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    __shared__ float wm[4];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+}
+
+__global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, const float* __restrict__ act) {
+    constexpr int T = 128, KS = 32;
+    constexpr int PLANE = T * KS * 2;   // bytes of one f16 [128][32] plane
+    __shared__ __attribute__((aligned(16))) char lds[2][4 * PLANE];   // stage: dY hi, dY lo, X hi, X lo
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.y * T, n0 = blockIdx.x * T;
+    const int M = a.Cout, N = a.ks * a.ks * a.Ctot;
+    const int tap = n0 / a.Ctot, ci0 = n0 - tap * a.Ctot;
+    const int ty = tap / a.ks, tx = tap - ty * a.ks;
+    const int kbeg = (int)(blockIdx.z * a.kspan), kend = (int)min(a.P, (int64_t)kbeg + a.kspan);   // P < 2^31
+    const int HWo = a.Hout * a.Wout;
+    const float sy = wg_scale(a.amax[0]), sx = wg_scale(a.amax[1]);
+    const int q = tid & 31, ko = tid >> 5;   // rows 4q..4q+3 (both operands), pixels 4ko..4ko+3 of a step
+    f4 yv[4], xv[4];   // [pixel]: 4 rows each
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int k = k0 + 4 * ko + p;
+            f4 y = f4{0.f, 0.f, 0.f, 0.f}, x = f4{0.f, 0.f, 0.f, 0.f};
+            if (k < kend) {
+                if (m0 + 4 * q < M) y = *(const f4*)(a.dy + (int64_t)k * M + m0 + 4 * q);
+                const int b = k / HWo;
+                const int rem = k - b * HWo;
+                const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+                int iy, ix;
+                bool ok;
+                if (a.up) {
+                    iy = oy - a.pad + ty;
+                    ix = ox - a.pad + tx;
+                    ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
+                    iy >>= 1;
+                    ix >>= 1;
+                } else {
+                    iy = oy * a.stride - a.pad + ty;
+                    ix = ox * a.stride - a.pad + tx;
+                    ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+                }
+                if (ok) {
+                    const int64_t pix = ((int64_t)b * a.Hin + iy) * a.Win + ix;
+                    const int ci = ci0 + 4 * q;
+                    if (act)
+                        x = *(const f4*)(act + pix * a.Ctot + ci);
+                    else
+                        x = ci < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + ci)
+                                      : *(const f4*)(a.src2 + pix * a.C2 + (ci - a.C1));
+                }
+            }
+            yv[p] = y;
+            xv[p] = x;
+        }
+    };
+    // transpose in registers: row r = 4q + i gets pixels 4ko..4ko+3 of both operands
+    auto store = [&](int buf) {
+        char* base = lds[buf];
+        const int off0 = (ko & 1) * 8;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int off = wg_swz(4 * q + i, ko >> 1) + off0;
+            uint2 hy, ly, hx, lx;
+            wg_split4(f4{yv[0][i], yv[1][i], yv[2][i], yv[3][i]}, sy, hy, ly);
+            wg_split4(f4{xv[0][i], xv[1][i], xv[2][i], xv[3][i]}, sx, hx, lx);
+            *(uint2*)(base + off) = hy;
+            *(uint2*)(base + PLANE + off) = ly;
+            *(uint2*)(base + 2 * PLANE + off) = hx;
+            *(uint2*)(base + 3 * PLANE + off) = lx;
+        }
+    };
+    f4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    const int li = lane & 15, g = lane >> 4;
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+        __syncthreads();
+        int cur = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += KS) {
+            const bool more = k0 + KS < kend;
+            if (more) load(k0 + KS);
+            const char* base = lds[cur];
+            h8v ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int off = wg_swz(wm * 64 + 16 * i + li, g);
+                ah[i] = *(const h8v*)(base + off);
+                al[i] = *(const h8v*)(base + PLANE + off);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int off = wg_swz(wn * 64 + 16 * j + li, g);
+                bh[j] = *(const h8v*)(base + 2 * PLANE + off);
+                bl[j] = *(const h8v*)(base + 3 * PLANE + off);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+            if (more) store(cur ^ 1);
+            __syncthreads();
+            cur ^= 1;
+        }
+    }
+    const float unscale = 1.f / (sx * sy);   // exact: a power of two
+    float* Cz = a.part + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + 16 * j + li;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * 64 + 16 * i + 4 * g + r;
+                if (m < M) Cz[(int64_t)m * N + n] = acc[i][j][r] * unscale;
+            }
+        }
+}
+
 // act (B, Hin, Win, Ctot) = the forward's GroupNorm affine (+ SiLU) of the two
 // sources, once per layer for conv_wgrad128_kernel (conv_wgrad_kernel's arithmetic)
 __global__ __launch_bounds__(256) void gn_act_kernel(WgradArgs a, int64_t nquads) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= nquads) return;
-    const int cqn = a.Ctot / 4;
-    const int64_t pix = i / cqn;
-    const int c = (int)(i - pix * cqn) * 4;
-    const int64_t b = pix / ((int64_t)a.Hin * a.Win);
-    f4 v = c < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c) : *(const f4*)(a.src2 + pix * a.C2 + (c - a.C1));
-    const float* s = a.ss + (b * a.Ctot + c) * 2;
+    float m = 0.f;
+    if (i < nquads) {
+        const int cqn = a.Ctot / 4;
+        const int64_t pix = i / cqn;
+        const int c = (int)(i - pix * cqn) * 4;
+        const int64_t b = pix / ((int64_t)a.Hin * a.Win);
+        f4 v = c < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c) : *(const f4*)(a.src2 + pix * a.C2 + (c - a.C1));
+        const float* s = a.ss + (b * a.Ctot + c) * 2;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        float x = v[j] * s[2 * j] + s[2 * j + 1];
-        if (a.silu) x = silu_f(x);
-        v[j] = x;
+        for (int j = 0; j < 4; ++j) {
+            float x = v[j] * s[2 * j] + s[2 * j + 1];
+            if (a.silu) x = silu_f(x);
+            v[j] = x;
+        }
+        *(f4*)(a.act + pix * a.Ctot + c) = v;
+        m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
     }
-    *(f4*)(a.act + pix * a.Ctot + c) = v;
+    if (a.amax_out) {   // the split weight gradient's operand range (absmax_kernel's reduction)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if ((threadIdx.x & 63) == 0) atomicMax(a.amax_out, __float_as_uint(m));
+    }
 }
 
 // G[co][ci][tap] (the reference weight layout) += sum_z part[z][co][tap * Ctot + ci]
@@ -545,17 +734,45 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
     CFD_REQUIRE(wgrad_part_floats(a) <= (size_t)a.part_cap, CFD_ESTATE, "internal: weight-gradient scratch");
     if (wgrad_fast(a)) {
         CFD_REQUIRE(a.P < (int64_t)1 << 31, CFD_ESHAPE, "weight gradient over 2^31 or more pixels");
+        // split-f16 products (CFD_WGRAD_SPLIT=0: the exact fp32-MFMA kernel)
+        static const int split_env = getenv("CFD_WGRAD_SPLIT") ? atoi(getenv("CFD_WGRAD_SPLIT")) : 1;
+        const bool split = split_env && a.amax_out;
+        unsigned* amax = a.amax_out;
+        auto absmax = [&](const float* x, int64_t n, unsigned* out) {
+            const int64_t n4 = n / 4;
+            hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(n4, 256)))),
+                               dim3(256), 0, st, x, n4, out);
+            check_launch("absmax_kernel");
+        };
+        if (split) {
+            CFD_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned), st));
+            absmax(a.dy, a.P * a.Cout, amax);
+        }
+        const int64_t srows = (int64_t)(a.P / ((int64_t)a.Hout * a.Wout)) * a.Hin * a.Win;
         const float* act = nullptr;
+        WgradArgs b = a;
+        b.amax_out = nullptr;
+        b.amax = amax;
         if (a.ss) {
             CFD_REQUIRE(a.act, CFD_ESTATE, "internal: activation scratch");
-            const int64_t nq = (int64_t)(a.P / ((int64_t)a.Hout * a.Wout)) * a.Hin * a.Win * (a.Ctot / 4);
-            hipLaunchKernelGGL(gn_act_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a, nq);
+            const int64_t nq = srows * (a.Ctot / 4);
+            WgradArgs g = a;
+            g.amax_out = split ? amax + 1 : nullptr;
+            hipLaunchKernelGGL(gn_act_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, g, nq);
             check_launch("gn_act_kernel");
             act = a.act;
+        } else if (split) {
+            absmax(a.src1, srows * a.C1, amax + 1);
+            if (a.src2 && a.C2) absmax(a.src2, srows * a.C2, amax + 1);
         }
         const dim3 grid((unsigned)(N / 128), (unsigned)ceil_div(a.Cout, 128), (unsigned)splits);
-        hipLaunchKernelGGL(conv_wgrad128_kernel, grid, dim3(256), 0, st, a, act);
-        check_launch("conv_wgrad128_kernel");
+        if (split) {
+            hipLaunchKernelGGL(conv_wgrad128_split_kernel, grid, dim3(256), 0, st, b, act);
+            check_launch("conv_wgrad128_split_kernel");
+        } else {
+            hipLaunchKernelGGL(conv_wgrad128_kernel, grid, dim3(256), 0, st, b, act);
+            check_launch("conv_wgrad128_kernel");
+        }
     } else {
         const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(a.Cout, 64), (unsigned)splits);
         hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, a);

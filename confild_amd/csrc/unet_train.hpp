@@ -17,6 +17,10 @@ struct WgradArgs {
     int C1, C2, Ctot, Cout;
     int Hin, Win, Hout, Wout;
     int ks, stride, pad, up, silu;
+    // split-f16 kernel: scratch for the two operand ranges (max |dY|, max |X| as
+    // float bits), written by the range pass and read by the product kernel
+    unsigned* amax_out;
+    const unsigned* amax;
 };
 
 // GroupNorm(+SiLU) parameter gradient partials

@@ -1,10 +1,11 @@
 """Launch-shape switches that must not change a single bit: they pick how the
-work is scheduled (register-ring depth of the K1s convolution tiles), never the
-tiles, their K order or the split-K boundaries, so every output's summation
-order -- and hence eps -- is unchanged.  Each setting runs in a child process
-(the switches are read once per process) over split-f16 U-Nets at the config-A
-and config-B widths, at batch 1 and 3 (the small-batch shapes the deeper rings
-are for), and the outputs are compared bit for bit with the default build."""
+work is scheduled -- the register-ring depth of the K1s convolution tiles
+(CFD_CONV_PF), the 64-channel small-batch workgroups of K1h / K1s (default,
+CFD_CONV_SMALLN=0 restores 128) -- never the tiles' K order or the split-K
+boundaries, so every output's summation order, and hence eps, is unchanged.
+Each setting runs in a child process (the switches are read once per process)
+over split-f16 U-Nets at the config-A and config-B widths, at batch 1 and 3 (the
+small-batch shapes these are for), compared bit for bit with the default."""
 import json
 import os
 import subprocess
@@ -42,7 +43,7 @@ def _run(env_extra):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3"])
+@pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0"])
 def test_schedule_switch_is_bit_identical(hip, knob):
     base = _run({})
     k, v = knob.split("=")

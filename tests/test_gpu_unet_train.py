@@ -78,6 +78,38 @@ def test_unet_param_grad_matches_autograd(hip, name):
     assert errs[0][0] < 2e-4, errs[:8]
 
 
+def test_unet_param_grad_split_is_fp32_level(hip):
+    """Split-f16 weight-gradient products (split compute, the default; every
+    convolution of wide128 runs them): each gradient tensor's error against a
+    float64 autograd evaluation stays within 2x the fp32 mode's (exact fp32-MFMA
+    products) + 1e-7 of the model's largest gradient -- the criterion the split
+    forward and input-gradient meet (test_gpu_unet_split.py, test_gpu_dps.py)."""
+    g, cfg, sd, m = _unet("wide128")
+    x = torch.from_numpy(g["x"])
+    t = torch.from_numpy(g["t"])
+    d_eps = torch.from_numpy(synth.normal(5, "wide128/deps", tuple(x.shape)))
+    params = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    eps_ref = ou.forward(params, cfg, x.double(), t)
+    ref = dict(zip(params.keys(), torch.autograd.grad(eps_ref, list(params.values()), d_eps.double())))
+    gmax = max(float(r.abs().max()) for r in ref.values())
+    named = dict(m.named_parameters())
+    err = {}
+    for mode in ("fp32", "split_f16"):
+        m.set_compute(mode)
+        m.forward_tape(x.to(DEV), t.to(DEV))
+        flat = m.param_grad(d_eps.to(DEV)).cpu().double()
+        o, e = 0, {}
+        for k in m.param_keys():
+            n = named[k].numel()
+            e[k] = float((flat[o:o + n].reshape(named[k].shape) - ref[k]).abs().max())
+            o += n
+        err[mode] = e
+    worst = sorted(((err["split_f16"][k] - 2 * err["fp32"][k]) / gmax, k) for k in err["fp32"])[-4:]
+    print(f"wide128 split vs fp32 gradient error (excess over 2x fp32, / max grad {gmax:.3e}): {worst}")
+    for k in err["fp32"]:
+        assert err["split_f16"][k] <= 2 * err["fp32"][k] + 1e-7 * gmax, (k, err["split_f16"][k], err["fp32"][k])
+
+
 def test_unet_param_grad_accumulates_and_is_deterministic(hip):
     g, cfg, sd, m = _unet("tiny16")
     x = torch.from_numpy(g["x"]).to(DEV)
