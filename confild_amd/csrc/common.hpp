@@ -57,6 +57,24 @@ typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 
 namespace cfd {
 
+// n / d for 0 <= n < 2^24, d >= 1, exact: a float multiply by r = RN(1/d) is
+// within one of the quotient, then one correction each way.  ~6 instructions
+// instead of the ~40 of an integer division by a runtime value -- the pixel
+// tables of the convolution prologues (measured in-kernel: ~1.4 us of a small
+// K1s launch was its table's divisions)
+__device__ __forceinline__ int fdiv24(int n, int d, float r) {
+    int q = (int)((float)n * r);
+    const int rm = n - q * d;
+    q += rm >= d ? 1 : 0;
+    q -= rm < 0 ? 1 : 0;
+    return q;
+}
+// tap / ks for the kernel sizes the convolutions use (3, 1, and the 4x4 and 2x2
+// of the input-gradient packs) without an integer division
+__device__ __forceinline__ int tap_row(int tap, int ks) {
+    return ks == 3 ? (tap * 11) >> 5 : ks == 4 ? tap >> 2 : ks == 2 ? tap >> 1 : ks == 1 ? 0 : tap / ks;
+}
+
 void set_error(const std::string& msg);
 
 struct Error {

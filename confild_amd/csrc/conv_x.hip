@@ -84,14 +84,15 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
     {
         const int ntap = a.ks * a.ks;
+        const float rhw = 1.0f / (float)HWo, rw = 1.0f / (float)a.Wout;   // fdiv24 (M < 2^24: launch_conv_x)
         for (int e = tid; e < ntap * BM; e += NT) {
             const int tap = e / BM, r = e - tap * BM;
-            const int ty = tap / a.ks, tx = tap - ty * a.ks;
+            const int ty = tap_row(tap, a.ks), tx = tap - ty * a.ks;
             const int m = m0 + r;
             int pix = -1;
             if (m < a.M) {
-                const int b = m / HWo, rem = m - b * HWo;
-                const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+                const int b = fdiv24(m, HWo, rhw), rem = m - b * HWo;
+                const int oy = fdiv24(rem, a.Wout, rw), ox = rem - oy * a.Wout;
                 int iy, ix;
                 bool ok;
                 if (a.up) {

@@ -273,8 +273,16 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     const int c = grp * cpg + 4 * q;
     const float* src = c < a.C1 ? a.src1 + b * HW * a.C1 + c : a.src2 + b * HW * a.C2 + (c - a.C1);
     const int ld = c < a.C1 ? a.C1 : a.C2;
-    __shared__ double red[2][NT];
+    constexpr int NWV = NT / 64;
+    __shared__ double wred[2][NWV];
     __shared__ float sh[2][32];
+    // this group's gamma / beta, loaded now (the finalize would otherwise wait one
+    // more memory latency for them after the reduction)
+    float gam = 0.f, bet = 0.f;
+    if (t < cpg) {
+        gam = a.gamma[grp * cpg + t];
+        bet = a.beta[grp * cpg + t];
+    }
     f4 v[IPT];
     bool ksrc = false;
     if constexpr (IPT <= 16) ksrc = a.kpart && c < a.C1;  // (gn_takes_splitk: IPT <= 16)
@@ -357,24 +365,33 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
             s += v[k][j];
             s2 += (double)v[k][j] * v[k][j];
         }
-    red[0][t] = s;
-    red[1][t] = s2;
-    __syncthreads();
-    for (int w = NT / 2; w > 0; w >>= 1) {  // fixed-order tree
-        if (t < w) {
-            red[0][t] += red[0][t + w];
-            red[1][t] += red[1][t + w];
-        }
-        __syncthreads();
+    // fixed-order reduction: a butterfly within each wave (lane 0's sum), then
+    // the NWV wave sums in wave order -- one barrier instead of a log2(NT)-level
+    // LDS tree (measured in-kernel: the tree was ~2-3 us of a 6-10 us GroupNorm)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o);
+        s2 += __shfl_xor(s2, o);
     }
+    if ((t & 63) == 0) {
+        wred[0][t >> 6] = s;
+        wred[1][t >> 6] = s2;
+    }
+    __syncthreads();
     if (t < cpg) {
+        double S = 0.0, S2 = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) {
+            S += wred[0][w];
+            S2 += wred[1][w];
+        }
         const double n = (double)HW * cpg;
-        const double mean = red[0][0] / n;
-        const double var = fmax(red[1][0] / n - mean * mean, 0.0);
+        const double mean = S / n;
+        const double var = fmax(S2 / n - mean * mean, 0.0);
         const float mf = (float)mean, rf = (float)(1.0 / sqrt(var + (double)a.eps));
         const int cc = grp * cpg + t;
-        const float sc = rf * a.gamma[cc];
-        const float sf = a.beta[cc] - mf * sc;
+        const float sc = rf * gam;
+        const float sf = bet - mf * sc;
         sh[0][t] = sc;
         sh[1][t] = sf;
         a.ss[(b * Ctot + cc) * 2 + 0] = sc;
@@ -591,14 +608,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
             b_voff[it] = n < a.Cout ? (unsigned)((n * a.K + 4 * kq) * WES) : 0x80000000u;
         }
         const int ntap = a.ks * a.ks;
+        const float rhw = 1.0f / (float)HWo, rw = 1.0f / (float)a.Wout;   // fdiv24 (M < 2^24: launch_conv)
         for (int e = tid; e < ntap * BM; e += 64 * NW) {
             const int tap = e / BM, r = e - tap * BM;
-            const int ty = tap / a.ks, tx = tap - ty * a.ks;
+            const int ty = tap_row(tap, a.ks), tx = tap - ty * a.ks;
             const int m = m0 + r;
             int pix = -1;
             if (m < a.M) {
-                const int b = m / HWo, rem = m - b * HWo;
-                const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+                const int b = fdiv24(m, HWo, rhw), rem = m - b * HWo;
+                const int oy = fdiv24(rem, a.Wout, rw), ox = rem - oy * a.Wout;
                 int iy, ix;
                 bool ok;
                 if (TMODE) {   // transposed addressing: dY[(o + pad - tap) / s] where divisible
@@ -1849,7 +1867,7 @@ void launch_splitk_reduce(const ConvArgs& a, int splits, hipStream_t st) {
 static bool conv_x_falls_back(const ConvArgs& a) {
     static const int force_k1s = env_int("CFD_CONV_FORCE_K1S", 0);
     const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
-    return force_k1s || !(srows < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31));
+    return force_k1s || !(srows < (1 << 24) && a.M < (1 << 24) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 31));
 }
 
 bool conv_runs_k1hb(const ConvArgs& a, const ConvPlan& p) { return p.kx == 22 && !conv_x_falls_back(a); }
@@ -1888,7 +1906,7 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     {   // 32-bit buffer offsets and 24-bit pixel indices must hold
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
         const int64_t wes = (a.wbf || a.wlo) ? 2 : 4;
-        b.bufaddr = bufaddr && a.ks * a.ks <= 9 && srows < (1 << 24) &&
+        b.bufaddr = bufaddr && a.ks * a.ks <= 9 && srows < (1 << 24) && a.M < (1 << 24) &&
                     srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * wes < (1ll << 31);
     }
     const ConvArgs& a_ = b;

@@ -238,8 +238,13 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(WgradArgs a, const f
 // in the K1s fragment layout; the next step's loads are in flight during the
 // MFMAs.  Partial slabs and wgrad_accum_kernel as in the fp32 kernel.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wg_swz(int row, int chunk) {   // unet_kernels.hip lds_swz_bf
-    return row * 64 + ((chunk + 2 * ((row >> 2) & 1)) & 3) * 16;
+// LDS byte offset of 16-B chunk `chunk` of operand row `row`: rows are permuted
+// within each group of 16 (bits 0-1 <-> bits 2-3) and the chunk is XOR-swizzled by
+// the row's low bits, so that both the transposing stores (a lane: rows 4q+i, one
+// 8-B half-chunk) and the fragment reads (16 rows x one chunk) spread over all banks
+__device__ __forceinline__ int wg_swz(int row, int chunk) {
+    const int P = (row & ~15) | ((row & 3) << 2) | ((row >> 2) & 3);
+    return P * 64 + ((chunk ^ row) & 3) * 16;
 }
 // hi = f16(s x), lo = f16(s x - hi) of 4 values, packed as 2 x (2 halfs)
 __device__ __forceinline__ void wg_split4(f4 x, float s, uint2& hi, uint2& lo) {
@@ -290,7 +295,8 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
     const int kbeg = (int)(blockIdx.z * a.kspan), kend = (int)min(a.P, (int64_t)kbeg + a.kspan);   // P < 2^31
     const int HWo = a.Hout * a.Wout;
     const float sy = wg_scale(a.amax[0]), sx = wg_scale(a.amax[1]);
-    const int q = tid & 31, ko = tid >> 5;   // rows 4q..4q+3 (both operands), pixels 4ko..4ko+3 of a step
+    const int q = tid >> 3, ko = tid & 7;   // rows 4q..4q+3 (both operands), pixels 4ko..4ko+3 of a step
+    const float rhw = 1.0f / (float)HWo, rw = 1.0f / (float)a.Wout;   // fdiv24: P < 2^24 (launch_conv_wgrad)
     f4 yv[4], xv[4];   // [pixel]: 4 rows each
     auto load = [&](int k0) {
 #pragma unroll
@@ -299,9 +305,9 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
             f4 y = f4{0.f, 0.f, 0.f, 0.f}, x = f4{0.f, 0.f, 0.f, 0.f};
             if (k < kend) {
                 if (m0 + 4 * q < M) y = *(const f4*)(a.dy + (int64_t)k * M + m0 + 4 * q);
-                const int b = k / HWo;
+                const int b = fdiv24(k, HWo, rhw);
                 const int rem = k - b * HWo;
-                const int oy = rem / a.Wout, ox = rem - oy * a.Wout;
+                const int oy = fdiv24(rem, a.Wout, rw), ox = rem - oy * a.Wout;
                 int iy, ix;
                 bool ok;
                 if (a.up) {
@@ -736,7 +742,7 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
         CFD_REQUIRE(a.P < (int64_t)1 << 31, CFD_ESHAPE, "weight gradient over 2^31 or more pixels");
         // split-f16 products (CFD_WGRAD_SPLIT=0: the exact fp32-MFMA kernel)
         static const int split_env = getenv("CFD_WGRAD_SPLIT") ? atoi(getenv("CFD_WGRAD_SPLIT")) : 1;
-        const bool split = split_env && a.amax_out;
+        const bool split = split_env && a.amax_out && a.P < (1 << 24);   // fdiv24 pixel decode
         unsigned* amax = a.amax_out;
         auto absmax = [&](const float* x, int64_t n, unsigned* out) {
             const int64_t n4 = n / 4;
