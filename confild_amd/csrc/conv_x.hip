@@ -765,9 +765,9 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         // workgroups of 8 waves, two per SIMD), 64-channel workgroups of 4 waves --
         // twice the workgroups, one wave per SIMD, the same tiles' sums
         // (CFD_CONV_SMALLN=0 keeps 128)
-        static const int smalln = getenv("CFD_CONV_SMALLN") ? atoi(getenv("CFD_CONV_SMALLN")) : 1;
+        static const int smalln = smalln_below();
         const dim3 g = grid(256, 128);
-        if (smalln && (int64_t)g.x * g.y * g.z < 128 && a.Cout % 64 == 0) {
+        if ((int64_t)g.x * g.y * g.z < smalln && a.Cout % 64 == 0) {
             const dim3 g64 = grid(256, 64);
             if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, false, false, 64>), g64, dim3(256), 0, st, a);
             else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, false, false, 64>), g64, dim3(256), 0, st, a);

@@ -1815,6 +1815,13 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     return p;
 }
 
+// grid size below which the K1s / K1h forward tiles go 64 channels wide
+// (CFD_CONV_SMALLN: 0 never, 1 the default 128 workgroups, n > 1 below n)
+int smalln_below() {
+    const int v = env_int("CFD_CONV_SMALLN", 1);
+    return v == 1 ? 128 : std::max(v, 0);
+}
+
 template <bool TMODE, int MODE, bool BUFA>
 static void launch_conv_tiles_(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
     if constexpr (!TMODE && MODE == 2 && BUFA) {   // the split-f16 forward
@@ -1822,8 +1829,8 @@ static void launch_conv_tiles_(const ConvArgs& a, const ConvPlan& p, dim3 grid, 
         // workgroups of 8 waves, two per SIMD), 128 x 64 tiles of 8 waves (32 x 32
         // each) -- twice the workgroups, half the work per wave, the same tiles'
         // sums (CFD_CONV_SMALLN=0 keeps 128 x 128)
-        static const int smalln = env_int("CFD_CONV_SMALLN", 1);
-        if (smalln && p.nw == 8 && p.bm == 128 && p.bn == 128 && (int64_t)grid.x * grid.y * grid.z < 128 &&
+        static const int smalln = smalln_below();
+        if (p.nw == 8 && p.bm == 128 && p.bn == 128 && (int64_t)grid.x * grid.y * grid.z < smalln &&
             a.Cout % 64 == 0) {
             const dim3 g64(grid.x, (unsigned)ceil_div(a.Cout, 64), grid.z);
             hipLaunchKernelGGL((conv_gemm_kernel<128, 64, false, 2, 8, true>), g64, dim3(512), 0, st, a);

@@ -160,6 +160,7 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st);
 int conv_h_tw(const ConvArgs& a);   // K1h tile width for a shape, 0: not applicable
 // whether launch_conv runs this plan on K1hb (the bf16 halo kernel, variant 22):
 // the only convolution that reads a bf16 source (ConvArgs::src_bf16)
+int smalln_below();
 bool conv_runs_k1hb(const ConvArgs& a, const ConvPlan& p);
 void launch_conv_in(const ConvArgs& a, hipStream_t st);
 void launch_conv_out(const ConvArgs& a, hipStream_t st);

@@ -160,8 +160,9 @@ def test_configE_100_consecutive_steps(hip, compute):
         assert max(es) <= 1e-5 and max(ex) <= 1e-4, (es, ex)
 
 
-# bf16 drift over the 100 steps (MI355X, round 4; set after the first measurement)
-BF16_SAMPLE_100, BF16_X0_100 = 2e-2, 5e-2
+# bf16 drift over the 100 steps, ~1.5x the measured worst (MI355X, round 4: sample
+# 7.2e-4 after 100 steps growing ~linearly from 9e-6 after 1; x0_hat 1.26e-2, flat)
+BF16_SAMPLE_100, BF16_X0_100 = 1.1e-3, 2e-2
 
 
 def test_configA_ddim50_and_decode_end_to_end(hip):

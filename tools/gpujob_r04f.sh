@@ -15,6 +15,12 @@ for spec in "--size 64 --batch 1" "--size 32 --mult 1,2,3,4 --batch 1" "--size 6
 CFD_LIB=$L timeout -k 10 200 python tools/kbench.py unet $spec > $O/kb.log 2>&1 || { cat $O/kb.log; exit 5; }
 echo "$L | $spec | $(grep kernel $O/kb.log | cut -c60-200)"
 done; done; done
+for r in 1 2; do
+for SN in 1 257 513; do
+for spec in "--size 64 --batch 8" "--size 64 --batch 4" "--size 32 --mult 1,2,3,4 --batch 8"; do
+CFD_CONV_SMALLN=$SN timeout -k 10 200 python tools/kbench.py unet $spec > $O/kb.log 2>&1 || { cat $O/kb.log; exit 5; }
+echo "SMALLN=$SN | $spec | $(grep kernel $O/kb.log | cut -c60-200)"
+done; done; done
 timeout -k 10 600 python -u -m pytest tests/test_gpu_unet_train.py -x -v -s --timeout 300 --timeout-method thread > $O/train_tests.log 2>&1 || { echo TRAINFAIL; grep -E "FAIL|Error|assert" $O/train_tests.log | head -20; tail -30 $O/train_tests.log; exit 3; }
 tail -1 $O/train_tests.log
 grep -E "wide128|worst|excess" $O/train_tests.log | head
