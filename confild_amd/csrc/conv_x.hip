@@ -460,12 +460,17 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs
         bvoff[it] = n < a.Cout ? (unsigned)((n * a.K + 8 * bq) * 2) : 0x80000000u;
     }
 
-    // this workgroup's chunks [c0, c1); group kg takes c0 + KG*r + kg in round r
+    // this workgroup's chunks [c0, c1); group kg takes the contiguous sub-range
+    // [c0 + kg * gper, cend), one chunk per round -- the ranges a split-K of
+    // gridDim.z * KG workgroups would give its splits, so with gridDim.z == 1 the
+    // group sums combined in group order are splitk_reduce's sums over the slabs
     const int nch = a.Ctot / 32;
     const int per = (nch + gridDim.z - 1) / gridDim.z;
     const int c0 = bz * per, c1 = min(nch, c0 + per);
-    const int nrounds = (max(c1 - c0, 0) + KG - 1) / KG;
-    auto chunk_of = [&](int r) { return c0 + KG * r + kg; };
+    const int gper = (max(c1 - c0, 0) + KG - 1) / KG;
+    const int cend = min(c1, c0 + (kg + 1) * gper);
+    const int nrounds = gper;
+    auto chunk_of = [&](int r) { return c0 + kg * gper + r; };
 
     typedef typename std::conditional<SB, uint2, f4>::type HT;   // one halo piece in registers
     HT rh[HIT];
@@ -518,7 +523,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs
     // step s = (round s / 9, tap s % 9)
     auto load_w = [&](int s, u4 (&rbh)[BIT], u4 (&rbl)[BIT]) {
         const int c = chunk_of(s / 9), t = s % 9;
-        if (c >= c1) return;
+        if (c >= cend) return;
         const int soff = (t * a.Ctot + 32 * c) * 2;
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
@@ -563,8 +568,8 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs
         const int r = s / 9, t = s - 9 * r;
         const int c = chunk_of(r);
         if (s + 2 < nsteps) load_w(s + 2, ldh, ldl);
-        if (t == 0 && chunk_of(r + 1) < c1) load_halo(chunk_of(r + 1));   // in registers until this chunk's taps are done
-        if (c < c1) {
+        if (t == 0 && chunk_of(r + 1) < cend) load_halo(chunk_of(r + 1));   // in registers until this chunk's taps are done
+        if (c < cend) {
             const int ty = t / 3;
             const int tofs = ty * HW2 + (t - 3 * ty);
             const char* wb = ring + (s & 1) * BSTAGE;
@@ -608,10 +613,10 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs
                     }
             }
         }
-        if (s + 1 < nsteps && chunk_of((s + 1) / 9) < c1) store_w((s + 1) & 1, sth, stl);
+        if (s + 1 < nsteps && chunk_of((s + 1) / 9) < cend) store_w((s + 1) & 1, sth, stl);
         __syncthreads();
         if (t == 8 && s + 1 < nsteps) {   // every wave is past the last tap of round r
-            if (chunk_of(r + 1) < c1) store_halo();
+            if (chunk_of(r + 1) < cend) store_halo();
             __syncthreads();
         }
     };
@@ -619,7 +624,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs
     if (nsteps > 0) {
         load_w(0, wx_h, wx_l);
         if (nsteps > 1) load_w(1, wy_h, wy_l);
-        if (chunk_of(0) < c1) {
+        if (chunk_of(0) < cend) {
             load_halo(chunk_of(0));
             store_w(0, wx_h, wx_l);
             store_halo();
@@ -633,6 +638,14 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs
     }
 
     CFD_STAMP(a.stamps, 3, a.seq, 3);
+    // undo the split weights' power-of-two scale (exact), per group before they
+    // are combined -- as the split-K slabs hold scaled sums
+    if constexpr (!BF) {   // undo the split weights' power-of-two scale (exact)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] *= a.acc_scale;
+    }
     // combine the K groups through LDS: groups 1.. park their sums, group 0 adds
     // them in group order (fixed summation order)
     if constexpr (KG > 1) {
@@ -670,12 +683,6 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs
         }
     }
 
-    if constexpr (!BF) {   // undo the split weights' power-of-two scale (exact)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] *= a.acc_scale;
-    }
     const int n_base = n0 + wn * 64 + l32;
     const int p_base = wm * 64 + 4 * hsel;   // tile position of acc element 0 of block 0
     auto pix_of = [&](int p) { return mrow0 + (int64_t)(p / TW) * W + (p % TW); };
@@ -757,7 +764,33 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         check_launch("conv_h_kernel");
         return splits;
     }
+    if (variant == 26) {   // K1hb with two in-workgroup K groups (the two splits of a split-K 2)
+        const int tw = conv_h_tw(a);
+        CFD_REQUIRE(tw > 0 && !a.wlo && splits == 1, CFD_ESHAPE, "conv_h bf16 K groups: 3x3 stride-1, no split-K");
+        const dim3 g = grid(256, 128);
+        if (a.src_bf16) {
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 2, true, true>), g, dim3(1024), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 2, true, true>), g, dim3(1024), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16, 2, true, true>), g, dim3(1024), 0, st, a);
+        } else {
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 2, true>), g, dim3(1024), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 2, true>), g, dim3(1024), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16, 2, true>), g, dim3(1024), 0, st, a);
+        }
+        check_launch("conv_h_kernel");
+        return 1;
+    }
     CFD_REQUIRE(!a.src_bf16, CFD_ESTATE, "internal: a bf16 convolution source needs the K1hb kernel");
+    if (variant == 24) {   // K1h with two in-workgroup K groups, 64 output channels (LDS: 2 x 67 KB at TW 64)
+        const int tw = conv_h_tw(a);
+        CFD_REQUIRE(tw > 0 && splits == 1 && a.Cout % 64 == 0, CFD_ESHAPE, "conv_h K groups: 3x3 stride-1, no split-K");
+        const dim3 g = grid(256, 64);
+        if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 2, false, false, 64>), g, dim3(512), 0, st, a);
+        else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 2, false, false, 64>), g, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_h_kernel<256, 16, 2, false, false, 64>), g, dim3(512), 0, st, a);
+        check_launch("conv_h_kernel");
+        return 1;
+    }
     if (variant == 20) {   // K1h: 256-pixel blocks
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0, CFD_ESHAPE, "conv_h: 3x3 stride-1 with a 16/32/64-divisible width");

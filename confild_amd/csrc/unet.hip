@@ -542,9 +542,12 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             fprintf(stderr, "CONV %s %dx%d C=%d+%d->%d ks=%d s=%d up=%d M=%d kx=%d bm=%d bn=%d nw=%d splits=%d\n",
                     pre.c_str(), a.Hin, a.Win, a.C1, a.C2, a.Cout, a.ks, a.stride, a.up, a.M, plan.kx, plan.bm,
                     plan.bn, plan.nw, plan.splits);
-        if (launch && cfd::launch_conv(a, plan, st, /*defer=*/true) > 1) {
-            pend.a = a;
-            pend.splits = plan.splits;
+        if (launch) {
+            const int sp = cfd::launch_conv(a, plan, st, /*defer=*/true);   // the splits it left to reduce
+            if (sp > 1) {
+                pend.a = a;
+                pend.splits = sp;
+            }
         }
     };
 

@@ -1917,6 +1917,16 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
                     srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * wes < (1ll << 31);
     }
     const ConvArgs& a_ = b;
+    // K1h / K1hb split-K 2 as two in-workgroup K groups (conv_x.hip): the same
+    // chunk ranges and combination order, so the same bits, without the partial
+    // slab and its reduction pass; where the grid keeps >= CFD_CONV_KHG workgroups
+    // (0: never)
+    static const int khg = env_int("CFD_CONV_KHG", 128);
+    if ((p.kx == 20 || p.kx == 22) && p.splits == 2 && khg > 0 && a.Cout % 64 == 0 &&
+        ceil_div(a.M, 256) * ceil_div(a.Cout, p.kx == 20 ? 64 : 128) >= khg) {
+        launch_conv_x(a_, p.kx + 4, 1, st);
+        return 1;
+    }
     if (p.kx >= 0) {
         launch_conv_x(a_, p.kx, p.splits, st);
         if (p.splits > 1 && !defer) launch_splitk_reduce(a, p.splits, st);

@@ -1,11 +1,15 @@
 """Launch-shape switches that must not change a single bit: they pick how the
 work is scheduled -- the register-ring depth of the K1s convolution tiles
 (CFD_CONV_PF), the 64-channel small-batch workgroups of K1h / K1s (default,
-CFD_CONV_SMALLN=0 restores 128) -- never the tiles' K order or the split-K
-boundaries, so every output's summation order, and hence eps, is unchanged.
-Each setting runs in a child process (the switches are read once per process)
-over split-f16 U-Nets at the config-A and config-B widths, at batch 1 and 3 (the
-small-batch shapes these are for), compared bit for bit with the default."""
+CFD_CONV_SMALLN=0 restores 128), the K1h / K1hb split-K 2 run as two
+in-workgroup K groups instead of two workgroups and a partial slab
+(CFD_CONV_KHG: 1 wherever it applies, 0 never; the default only above 128
+workgroups) -- never the tiles' K order or the split-K boundaries, so every
+output's summation order, and hence eps, is unchanged.  Each setting runs in a
+child process (the switches are read once per process) over split-f16 U-Nets at
+the config-A and config-B widths, at batch 1 and 3 (the small-batch shapes these
+are for), and bf16 (config-E arithmetic) U-Nets with bf16 GroupNorm outputs,
+compared bit for bit with the default."""
 import json
 import os
 import subprocess
@@ -32,6 +36,15 @@ for S, mult in ((32, "1,2,3,4"), (64, "")):
         x = torch.from_numpy(synth.normal(4, f"knob/x{S}", (B, 1, S, S))).cuda()
         t = torch.tensor([999, 400, 3][:B], dtype=torch.int64).cuda()
         out[f"{S}/{B}"] = m(x, t).cpu().numpy().tobytes().hex()
+for S, mult in ((32, "1,2,2"), (64, "")):
+    m = create_model(image_size=S, num_channels=128, num_res_blocks=2, channel_mult=mult, num_heads=4,
+                     num_head_channels=64, attention_resolutions="32,16,8", use_bf16=True)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in
+                       synth.unet_state_dict(12, {k: tuple(v.shape) for k, v in m.state_dict().items()}).items()})
+    m.to("cuda")
+    x = torch.from_numpy(synth.normal(5, f"knob/xb{S}", (2, 1, S, S))).cuda()
+    t = torch.tensor([999, 3], dtype=torch.int64).cuda()
+    out[f"bf16/{S}"] = m(x, t).cpu().numpy().tobytes().hex()
 print(json.dumps(out))
 """
 
@@ -43,7 +56,8 @@ def _run(env_extra):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0"])
+@pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0", "CFD_CONV_KHG=1",
+                                  "CFD_CONV_KHG=0"])
 def test_schedule_switch_is_bit_identical(hip, knob):
     base = _run({})
     k, v = knob.split("=")
