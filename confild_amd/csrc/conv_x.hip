@@ -735,8 +735,8 @@ int conv_h_tw(const ConvArgs& a) {
 }
 
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
-    CFD_REQUIRE(a.wbf && (a.wlo || variant == 22) && !a.tmode, CFD_ESTATE,
-                "conv_x: split-f16 forward only (variant 22: bf16)");
+    CFD_REQUIRE(a.wbf && (a.wlo || variant == 22 || variant == 26) && !a.tmode, CFD_ESTATE,
+                "conv_x: split-f16 forward only (variants 22 / 26: bf16)");
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_x needs channels % 32 == 0");
     CFD_REQUIRE(splits == 1 || a.part, CFD_ESTATE, "split-K needs a partial buffer");
     {   // K1x / K1h: 32-bit buffer offsets, 24-bit pixel indices
