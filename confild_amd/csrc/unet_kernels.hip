@@ -1921,7 +1921,7 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     // chunk ranges and combination order, so the same bits, without the partial
     // slab and its reduction pass; where the grid keeps >= CFD_CONV_KHG workgroups
     // (0: never)
-    static const int khg = env_int("CFD_CONV_KHG", 128);
+    static const int khg = env_int("CFD_CONV_KHG", 0);
     if ((p.kx == 20 || p.kx == 22) && p.splits == 2 && khg > 0 && a.Cout % 64 == 0 &&
         ceil_div(a.M, 256) * ceil_div(a.Cout, p.kx == 20 ? 64 : 128) >= khg) {
         launch_conv_x(a_, p.kx + 4, 1, st);

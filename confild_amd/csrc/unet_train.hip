@@ -410,10 +410,9 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
 // act (B, Hin, Win, Ctot) = the forward's GroupNorm affine (+ SiLU) of the two
 // sources, once per layer for conv_wgrad128_kernel (conv_wgrad_kernel's arithmetic)
 __global__ __launch_bounds__(256) void gn_act_kernel(WgradArgs a, int64_t nquads) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     float m = 0.f;
-    if (i < nquads) {
-        const int cqn = a.Ctot / 4;
+    const int cqn = a.Ctot / 4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nquads; i += (int64_t)gridDim.x * 256) {
         const int64_t pix = i / cqn;
         const int c = (int)(i - pix * cqn) * 4;
         const int64_t b = pix / ((int64_t)a.Hin * a.Win);
@@ -426,12 +425,15 @@ __global__ __launch_bounds__(256) void gn_act_kernel(WgradArgs a, int64_t nquads
             v[j] = x;
         }
         *(f4*)(a.act + pix * a.Ctot + c) = v;
-        m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     }
-    if (a.amax_out) {   // the split weight gradient's operand range (absmax_kernel's reduction)
+    if (a.amax_out) {   // the split weight gradient's operand range: one atomic per workgroup
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        if ((threadIdx.x & 63) == 0) atomicMax(a.amax_out, __float_as_uint(m));
+        __shared__ float wm[4];
+        if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(a.amax_out, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
     }
 }
 
@@ -764,7 +766,8 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
             const int64_t nq = srows * (a.Ctot / 4);
             WgradArgs g = a;
             g.amax_out = split ? amax + 1 : nullptr;
-            hipLaunchKernelGGL(gn_act_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, g, nq);
+            hipLaunchKernelGGL(gn_act_kernel, dim3((unsigned)std::min<int64_t>(4096, ceil_div(nq, 256))), dim3(256), 0, st,
+                               g, nq);
             check_launch("gn_act_kernel");
             act = a.act;
         } else if (split) {
