@@ -36,11 +36,14 @@ __device__ __forceinline__ void cfd_stamp(unsigned long long* buf, unsigned kind
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
         const unsigned long long i = atomicAdd(buf, 1ULL);
         if (i < (1ull << 20)) {
-            unsigned long long* r = buf + 8 + 4 * i;
+            unsigned long long* r = buf + 8 + 8 * i;
             r[0] = t;
             r[1] = ((unsigned long long)kind << 56) | ((unsigned long long)seq << 24) | slot;
             r[2] = blockIdx.x + ((unsigned long long)blockIdx.y << 20) + ((unsigned long long)blockIdx.z << 40);
             r[3] = __builtin_amdgcn_s_memtime();
+            // where the wave runs: HW_ID (hwreg 4: simd, cu, sh, se) and XCC_ID (hwreg 20), read-only
+            r[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                   ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
         }
     }
 }

@@ -386,8 +386,10 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // copied to LDS as they are -- half the activation bytes, the same bits.
 // BN: output channels per workgroup, 128 (two wave columns) or 64 (one: at small
 // batch twice the workgroups, one wave per SIMD -- the same tiles' sums)
-template <int BM, int TW, int KG = 1, bool BF = false, bool SB = false, int BN = 128>
-__global__ __launch_bounds__(BM * (BN / 64) * KG, 1) void conv_h_kernel(ConvArgs a) {
+// OCC: waves per SIMD the register allocation must allow (launch bound) -- 4 lets
+// two 8-wave K1hb workgroups share a CU where the grid has more than one per CU
+template <int BM, int TW, int KG = 1, bool BF = false, bool SB = false, int BN = 128, int OCC = 1>
+__global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvArgs a) {
     static_assert(!SB || BF, "a bf16 source needs the bf16 kernel");
     constexpr unsigned SES = SB ? 2u : 4u;   // source element bytes
     constexpr int WGN = BN / 64, WGM = BM / 64, NTG = 64 * WGM * WGN;   // threads per K group (the workgroup: NTG * KG)
@@ -752,6 +754,17 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0 && !a.wlo, CFD_ESHAPE, "conv_h bf16: 3x3 stride-1 with a 16/32/64-divisible width");
         const dim3 g = grid(256, 128);
+        // more than one workgroup per CU: the 4-waves-per-SIMD build (two per CU) where
+        // CFD_CONV_KHB_OCC (development) asks for it
+        static const int occ = getenv("CFD_CONV_KHB_OCC") ? atoi(getenv("CFD_CONV_KHB_OCC")) : 0;
+        if (occ && tw == 64 && (int64_t)g.x * g.y * g.z > 256) {
+            if (a.src_bf16)
+                hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true, true, 128, 4>), g, dim3(512), 0, st, a);
+            else
+                hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true, false, 128, 4>), g, dim3(512), 0, st, a);
+            check_launch("conv_h_kernel");
+            return splits;
+        }
         if (a.src_bf16) {
             if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true, true>), g, dim3(512), 0, st, a);
             else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, true, true>), g, dim3(512), 0, st, a);
