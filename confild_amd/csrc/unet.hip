@@ -85,6 +85,8 @@ struct cfd_unet {
     float* rp_part = nullptr;      // (nblocks, 2) per-block |max| (forward pack, input-gradient pack)
     float* rp_amax = nullptr;      // (nparams, 2)
     int64_t rp_blocks = 0;
+    int64_t* rp_tfirst = nullptr;  // (nparams + 1) first transposing tile of each parameter
+    int64_t rp_tiles = 0;
 };
 
 namespace {
@@ -1091,6 +1093,7 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->rp_first);
     (void)hipFree(h->rp_part);
     (void)hipFree(h->rp_amax);
+    (void)hipFree(h->rp_tfirst);
     delete h;
 }
 
@@ -1370,15 +1373,59 @@ __global__ __launch_bounds__(256) void rp_pack_kernel(const float* __restrict__ 
                 rp_split(v, s, arena_hi, arena_lo, d.off + e);
             }
         }
-        if (conv && d.tpack && e < d.tcount) {
+        (void)conv;
+        (void)ts;   // the input-gradient packs: rp_tpack_kernel
+    }
+}
+
+// The input-gradient packs of the convolution weights, src (o, i, tap) ->
+// dst (i, tap', o) (tap' = tap, or taps - 1 - tap: tpack 1 / 3) or the 4x4 upsample
+// pack dst (i, q, o) (tpack 2, rp_up_value): o is fastest in the destination and
+// slowest in the source, so a workgroup stages a 64 (o) x RP_TI (i) x taps block of
+// the source in LDS (rows of contiguous (i, tap) runs, coalesced) and writes the
+// destination rows 64 o at a time (coalesced) -- the same values, the same sums
+constexpr int RP_TI = 8;
+__global__ __launch_bounds__(256) void rp_tpack_kernel(const float* __restrict__ flat,
+                                                       const RepackDesc* __restrict__ desc,
+                                                       const int64_t* __restrict__ tfirst, int np,
+                                                       const float* __restrict__ amax, float* __restrict__ arena_t,
+                                                       _Float16* __restrict__ arena_thi,
+                                                       _Float16* __restrict__ arena_tlo) {
+    const int64_t blk = blockIdx.x;
+    const int p = rp_param(tfirst, np, blk);
+    const RepackDesc d = desc[p];
+    const float* w = flat + d.src;
+    const int64_t tile = blk - tfirst[p];
+    const int nti = (d.ci + RP_TI - 1) / RP_TI;
+    const int o0 = (int)(tile / nti) * 64, i0 = (int)(tile % nti) * RP_TI;
+    const int taps = d.taps, run = RP_TI * taps, ld = run + 1;
+    __shared__ float tl[64 * (RP_TI * 9 + 1)];
+    for (int e = threadIdx.x; e < 64 * run; e += 256) {
+        const int ol = e / run, c = e - ol * run;
+        const int o = o0 + ol, i = i0 + c / taps;
+        tl[ol * ld + c] = o < d.co && i < d.ci ? w[((int64_t)o * d.ci + i0) * taps + c] : 0.f;
+    }
+    __syncthreads();
+    const float ts = rp_scale(amax[p * 2 + 1]);
+    const int ol = threadIdx.x & 63, o = o0 + ol;
+    const int nq = d.tpack == 2 ? 16 : taps;   // destination rows per i
+    if (o < d.co) {
+        for (int r = threadIdx.x >> 6; r < RP_TI * nq; r += 4) {
+            const int il = r / nq, q = r - il * nq, i = i0 + il;
+            if (i >= d.ci) break;
+            const float* src = tl + ol * ld + il * taps;
             float v;
-            if (d.tpack == 2) {
-                v = rp_up_value(w, d, e);
-            } else {   // dst (i, tap', o) <- src (o, i, tap), tap' = tap (1) or taps - 1 - tap (3)
-                const int64_t o = e % d.co, r = e / d.co, tt = r % d.taps, i = r / d.taps;
-                const int64_t tap = d.tpack == 3 ? d.taps - 1 - tt : tt;
-                v = w[(o * d.ci + i) * d.taps + tap];
+            if (d.tpack == 2) {   // rp_up_value's taps in its order
+                const int ey = q >> 2, ex = q & 3;
+                const int dlo_y = ey == 0 ? 2 : ey == 1 ? 1 : 0, dhi_y = ey == 0 ? 2 : ey == 1 ? 2 : ey == 2 ? 1 : 0;
+                const int dlo_x = ex == 0 ? 2 : ex == 1 ? 1 : 0, dhi_x = ex == 0 ? 2 : ex == 1 ? 2 : ex == 2 ? 1 : 0;
+                v = 0.f;
+                for (int dy = dlo_y; dy <= dhi_y; ++dy)
+                    for (int dx = dlo_x; dx <= dhi_x; ++dx) v += src[dy * 3 + dx];
+            } else {
+                v = src[d.tpack == 3 ? taps - 1 - q : q];
             }
+            const int64_t e = ((int64_t)i * nq + q) * d.co + o;
             arena_t[d.toff + e] = v;
             rp_split(v, ts, arena_thi, arena_tlo, d.toff + e);
         }
@@ -1420,6 +1467,22 @@ extern "C" int cfd_unet_load_flat(cfd_unet* h, const float* flat, size_t n, void
                 src += d.count;
             }
             first[np] = blocks;
+            std::vector<int64_t> tfirst(np + 1);
+            int64_t tiles = 0;
+            for (int k = 0; k < np; ++k) {
+                const auto& d = desc[k];
+                const bool conv = d.pack == (int)Pack::Conv1 || d.pack == (int)Pack::Conv3;
+                tfirst[k] = tiles;
+                if (conv && d.tpack) {
+                    CFD_REQUIRE(d.taps <= 9 && (int64_t)d.co * d.ci * d.taps == d.count, CFD_ESTATE,
+                                "internal: input-gradient pack shape");
+                    tiles += cfd::ceil_div(d.co, 64) * cfd::ceil_div(d.ci, cfd::RP_TI);
+                }
+            }
+            tfirst[np] = tiles;
+            CFD_HIP(hipMalloc(&h->rp_tfirst, sizeof(int64_t) * (np + 1)));
+            CFD_HIP(hipMemcpy(h->rp_tfirst, tfirst.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice));
+            h->rp_tiles = tiles;
             CFD_HIP(hipMalloc(&h->rp_desc, sizeof(cfd::RepackDesc) * np));
             CFD_HIP(hipMalloc(&h->rp_first, sizeof(int64_t) * (np + 1)));
             CFD_HIP(hipMalloc(&h->rp_part, sizeof(float) * 2 * blocks));
@@ -1439,6 +1502,12 @@ extern "C" int cfd_unet_load_flat(cfd_unet* h, const float* flat, size_t n, void
                            (_Float16*)h->arena_lo, h->arena_t, (_Float16*)h->arena_thi, (_Float16*)h->arena_tlo,
                            h->emb_w, h->emb_b, h->tdim);
         cfd::check_launch("rp_pack_kernel");
+        if (h->rp_tiles) {
+            hipLaunchKernelGGL(cfd::rp_tpack_kernel, dim3((unsigned)h->rp_tiles), dim3(256), 0, st, flat, desc,
+                               h->rp_tfirst, np, h->rp_amax, h->arena_t, (_Float16*)h->arena_thi,
+                               (_Float16*)h->arena_tlo);
+            cfd::check_launch("rp_tpack_kernel");
+        }
         std::vector<float> amax(2 * (size_t)np);
         CFD_HIP(hipMemcpyAsync(amax.data(), h->rp_amax, sizeof(float) * 2 * np, hipMemcpyDeviceToHost, st));
         CFD_HIP(hipStreamSynchronize(st));
