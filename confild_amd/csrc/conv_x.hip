@@ -722,6 +722,10 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                 a.out[(int64_t)m * a.Cout + n] = v;
             }
         }
+#ifdef CFD_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    CFD_STAMP(a.stamps, 3, a.seq, 4);
 }
 
 // K1h tile width for this shape (0: K1h does not apply): the widest of 64, 32,
@@ -754,9 +758,12 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0 && !a.wlo, CFD_ESHAPE, "conv_h bf16: 3x3 stride-1 with a 16/32/64-divisible width");
         const dim3 g = grid(256, 128);
-        // more than one workgroup per CU: the 4-waves-per-SIMD build (two per CU) where
-        // CFD_CONV_KHB_OCC (development) asks for it
-        static const int occ = getenv("CFD_CONV_KHB_OCC") ? atoi(getenv("CFD_CONV_KHB_OCC")) : 0;
+        // more than one workgroup per CU (the 128^2 level of config E): the build
+        // whose registers allow 4 waves per SIMD, two workgroups per CU instead of
+        // one (11-30 values spilled, loop-invariant; measured: 128^2 launches 70-88
+        // -> 47 us, config-E forward 5.87 -> 5.47 ms).  Same arithmetic, same bits;
+        // CFD_CONV_KHB_OCC=0 keeps the 3-waves build.
+        static const int occ = getenv("CFD_CONV_KHB_OCC") ? atoi(getenv("CFD_CONV_KHB_OCC")) : 1;
         if (occ && tw == 64 && (int64_t)g.x * g.y * g.z > 256) {
             if (a.src_bf16)
                 hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true, true, 128, 4>), g, dim3(512), 0, st, a);

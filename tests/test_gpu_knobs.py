@@ -3,8 +3,9 @@ work is scheduled -- the register-ring depth of the K1s convolution tiles
 (CFD_CONV_PF), the 64-channel small-batch workgroups of K1h / K1s (default,
 CFD_CONV_SMALLN=0 restores 128), the K1h / K1hb split-K 2 run as two
 in-workgroup K groups instead of two workgroups and a partial slab
-(CFD_CONV_KHG: 1 wherever it applies, 0 never; the default only above 128
-workgroups) -- never the tiles' K order or the split-K boundaries, so every
+(CFD_CONV_KHG: 1 wherever it applies; default 0, never), the K1hb register
+build for two workgroups per CU (CFD_CONV_KHB_OCC, default on above 256
+workgroups: the 128^2 batch-5 case) -- never the tiles' K order or the split-K boundaries, so every
 output's summation order, and hence eps, is unchanged.  Each setting runs in a
 child process (the switches are read once per process) over split-f16 U-Nets at
 the config-A and config-B widths, at batch 1 and 3 (the small-batch shapes these
@@ -36,14 +37,14 @@ for S, mult in ((32, "1,2,3,4"), (64, "")):
         x = torch.from_numpy(synth.normal(4, f"knob/x{S}", (B, 1, S, S))).cuda()
         t = torch.tensor([999, 400, 3][:B], dtype=torch.int64).cuda()
         out[f"{S}/{B}"] = m(x, t).cpu().numpy().tobytes().hex()
-for S, mult in ((32, "1,2,2"), (64, "")):
+for S, mult, B in ((32, "1,2,2", 2), (64, "", 2), (128, "1,1", 5)):
     m = create_model(image_size=S, num_channels=128, num_res_blocks=2, channel_mult=mult, num_heads=4,
                      num_head_channels=64, attention_resolutions="32,16,8", use_bf16=True)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in
                        synth.unet_state_dict(12, {k: tuple(v.shape) for k, v in m.state_dict().items()}).items()})
     m.to("cuda")
-    x = torch.from_numpy(synth.normal(5, f"knob/xb{S}", (2, 1, S, S))).cuda()
-    t = torch.tensor([999, 3], dtype=torch.int64).cuda()
+    x = torch.from_numpy(synth.normal(5, f"knob/xb{S}", (B, 1, S, S))).cuda()
+    t = torch.tensor([999, 3, 500, 40, 700][:B], dtype=torch.int64).cuda()
     out[f"bf16/{S}"] = m(x, t).cpu().numpy().tobytes().hex()
 print(json.dumps(out))
 """
@@ -57,7 +58,7 @@ def _run(env_extra):
 
 
 @pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0", "CFD_CONV_KHG=1",
-                                  "CFD_CONV_KHG=0"])
+                                  "CFD_CONV_KHB_OCC=0"])
 def test_schedule_switch_is_bit_identical(hip, knob):
     base = _run({})
     k, v = knob.split("=")
