@@ -688,6 +688,55 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     const int n_base = n0 + wn * 64 + l32;
     const int p_base = wm * 64 + 4 * hsel;   // tile position of acc element 0 of block 0
     auto pix_of = [&](int p) { return mrow0 + (int64_t)(p / TW) * W + (p % TW); };
+    if constexpr (KG == 1) {
+        // epilogue through LDS (launch_conv's ldsepi: Cout % 4 == 0, 16-B rows): one
+        // 64-pixel wave row of the tile at a time is parked in LDS and leaves as
+        // float4 row pieces, bias / emb / residual read the same way -- instead of
+        // 4-byte accesses two 128-B pieces per instruction (measured at config E's
+        // 128^2 level: the epilogue was 19-39 us of a 60-80 us workgroup).  The
+        // same adds in the same order: the same bits.
+        if (a.ldsepi) {
+            static_assert(64 * BN * 4 <= (int)sizeof(lds), "epilogue stage fits the LDS");
+            float* stg = (float*)lds;
+            const bool split = gridDim.z > 1;
+            float* dstb = split ? a.part + (int64_t)bz * a.M * a.Cout : a.out;
+            constexpr int Q = BN / 4;   // float4 pieces per staged pixel row
+            __syncthreads();            // every wave is past its last halo / ring read
+            for (int r = 0; r < WGM; ++r) {
+                if (wm == r) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e)
+#pragma unroll
+                            for (int j = 0; j < 2; ++j)
+                                stg[(32 * i + 8 * (e >> 2) + (e & 3) + 4 * hsel) * BN + wn * 64 + 32 * j + l32] =
+                                    acc[i][j][e];
+                }
+                __syncthreads();
+                for (int q = tid; q < 64 * Q; q += NTG) {
+                    const int p = q / Q, c = (q - p * Q) * 4;
+                    const int n = n0 + c;
+                    if (n < a.Cout) {
+                        const int64_t m = pix_of(r * 64 + p);
+                        f4 v = *(const f4*)(stg + p * BN + c);
+                        if (!split) {
+                            if (a.bias) v = v + *(const f4*)(a.bias + n);
+                            if (a.emb) v = v + *(const f4*)(a.emb + (int64_t)bimg * a.emb_stride + n);
+                            if (a.res) v = *(const f4*)(a.res + m * a.Cout + n) + v;
+                        }
+                        *(f4*)(dstb + m * a.Cout + n) = v;
+                    }
+                }
+                __syncthreads();
+            }
+#ifdef CFD_STAMPS
+            __builtin_amdgcn_s_waitcnt(0);
+#endif
+            CFD_STAMP(a.stamps, 3, a.seq, 4);
+            return;
+        }
+    }
     if (gridDim.z > 1) {
         float* part = a.part + (int64_t)bz * a.M * a.Cout;
 #pragma unroll
