@@ -70,7 +70,7 @@ METRIC = "generated fields/sec (256-step sample + CNF decode), Case4 latent, 1/2
 #   (kernel name, peak in algorithmic fp32 TFLOP/s, basis, committed PMC record)
 ROOFLINE = {
     "split_f16": ("siren_split32", F16_PEAK_TFLOPS / 3,
-                  "f16 dense MFMA peak / 3 (three f16 MFMAs per fp32 product)", "r02_siren_split32_pmc.json"),
+                  "f16 dense MFMA peak / 3 (three f16 MFMAs per fp32 product)", "r04_siren_split32_pmc.json"),
     "f32": ("siren_fused", FMA_PEAK_TFLOPS, "fp32 MFMA peak", "r01_siren_pmc.json"),
 }
 
@@ -95,13 +95,13 @@ def measured_mfma_util(kname):
     """Matrix-pipe busy fraction and held clock from the committed rocprofv3 record
     (tools/gpujob_mfma_util.sh, tools/mfma_util.py)."""
     try:
-        rec = json.load(open(os.path.join(ROOT, "profiles", "r02_mfma_util.json")))
+        rec = json.load(open(os.path.join(ROOT, "profiles", "r04_mfma_util.json")))
     except (OSError, ValueError):
         return None
     for k, v in rec.items():
         if k.startswith(f"cfd::{kname}<") and isinstance(v, dict):
             return {"mfma_busy_frac": v["mfma_busy_frac"], "held_clock_ghz": v["held_clock_ghz"],
-                    "source": "profiles/r02_mfma_util.json"}
+                    "source": "profiles/r04_mfma_util.json"}
     return None
 
 
