@@ -503,7 +503,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     __shared__ __attribute__((aligned(16))) float smem_ab[2 * AFL + 2 * BFL];
     float(*const As)[AFL] = (float(*)[AFL])smem_ab;
     float(*const Bs)[BFL] = (float(*)[BFL])(smem_ab + 2 * AFL);
-    constexpr bool LDSEPI_FITS = !BF && BM * BN <= 2 * AFL + 2 * BFL;
+    // the LDS epilogue parks the BM x BN tile in EPI_PASSES row bands (bf16 tiles
+    // leave half the fp32 tile's LDS: two bands of whole wave rows)
+    constexpr int EPI_FL = 2 * AFL + 2 * BFL;
+    constexpr int EPI_PASSES = (BM * BN + EPI_FL - 1) / EPI_FL;
+    constexpr bool LDSEPI_FITS = BM % EPI_PASSES == 0 && (BM / EPI_PASSES) % WM == 0 &&
+                                 (BM / EPI_PASSES) * BN <= EPI_FL && (BM / EPI_PASSES) * BN / 4 % (64 * NW) == 0;
     // buffer-addressed forward (a.bufaddr): source pixel of every (tap, tile row),
     // -1 for padding, built once per workgroup; the tile loads then cost one table
     // read, one 24-bit multiply-add and a select per row instead of the 64-bit
@@ -859,24 +864,28 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     // write land in different banks.  Same values, same rounding.
     if constexpr (LDSEPI_FITS) {
         if (a.ldsepi) {
+          constexpr int RB = BM / EPI_PASSES;   // tile rows per band
+          for (int band = 0; band < EPI_PASSES; ++band) {
             __syncthreads();
             float* tile = smem_ab;
             auto sw = [](int row, int col) { return row * BN + (col ^ (((row >> 2) & 3) << 4)); };
+            if (wm * WM / RB == band) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
+                    for (int j = 0; j < TN; ++j)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        tile[sw(wm * WM + 16 * i + g4 + r, wn * WN + 16 * j + li)] = acc[i][j][r];
+                        for (int r = 0; r < 4; ++r)
+                            tile[sw(wm * WM - band * RB + 16 * i + g4 + r, wn * WN + 16 * j + li)] = acc[i][j][r];
+            }
             __syncthreads();
-            constexpr int NV = BM * BN / 4 / (64 * NW);
+            constexpr int NV = RB * BN / 4 / (64 * NW);
             float* part = gridDim.z > 1 ? a.part + (int64_t)bz * a.M * a.Cout : nullptr;
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
                 const int idx = tid + v * 64 * NW;
                 const int row = idx / (BN / 4), c4 = (idx - row * (BN / 4)) * 4;
-                const int m = m0 + row, n = n0 + c4;
+                const int m = m0 + band * RB + row, n = n0 + c4;
                 if (m >= a.M || n >= a.Cout) continue;
                 f4 val = *(const f4*)&tile[sw(row, c4)];
                 const int64_t o = (int64_t)m * a.Cout + n;
@@ -889,6 +898,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                 if (a.res) val = *(const f4*)(a.res + o) + val;
                 *(f4*)(a.out + o) = val;
             }
+          }
 #ifdef CFD_STAMPS
             __builtin_amdgcn_s_waitcnt(0);
 #endif
