@@ -715,7 +715,11 @@ int64_t wgrad_kspan(const WgradArgs& a) {
     if (wgrad_fast(a)) {
         const int64_t N = (int64_t)a.ks * a.ks * a.Ctot, MN = (int64_t)a.Cout * N;
         const int64_t tiles = ceil_div(N, 128) * ceil_div(a.Cout, 128);
-        splits = std::min<int64_t>({64, ceil_div(2048, tiles), ceil_div(a.P, 256), std::max<int64_t>(1, a.part_cap / MN)});
+        // development: CFD_WGRAD_SMAX / CFD_WGRAD_TARGET (slices at most / block target)
+        static const int smax = getenv("CFD_WGRAD_SMAX") ? atoi(getenv("CFD_WGRAD_SMAX")) : 64;
+        static const int target = getenv("CFD_WGRAD_TARGET") ? atoi(getenv("CFD_WGRAD_TARGET")) : 2048;
+        splits = std::min<int64_t>({(int64_t)smax, ceil_div(target, tiles), ceil_div(a.P, 256),
+                                    std::max<int64_t>(1, a.part_cap / MN)});
         splits = std::max<int64_t>(1, splits);
         const int64_t span = ceil_div(a.P, splits);
         return (span + 31) / 32 * 32;

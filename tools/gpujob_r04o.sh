@@ -11,3 +11,7 @@ echo "LDSEPI=$EP | E | $(grep kernel $O/kb.log | cut -c60-200)"
 done; done
 CFD_LIB=libconfild_hip_stamps.so timeout -k 10 200 python tools/dev/stamps.py --size 128 --batch 8 --bf16 --detail 400 > $O/e128b8.txt 2>&1 || { tail -20 $O/e128b8.txt; exit 3; }
 tail -4 $O/e128b8.txt
+for SM in 64 128 256; do
+CFD_WGRAD_SMAX=$SM CFD_WGRAD_TARGET=8192 timeout -k 10 300 python3 tools/kbench.py utrain --batch 16 --size 128 > $O/ut$SM.out 2> $O/ut$SM.err || { tail -20 $O/ut$SM.err; exit 4; }
+echo "WGRAD_SMAX=$SM $(grep unet_train_step $O/ut$SM.out | cut -c1-330)"
+done
