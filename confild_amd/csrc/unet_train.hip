@@ -708,17 +708,20 @@ bool wgrad_fast(const WgradArgs& a) {
 }  // namespace
 
 // pixel slices: the 64-tile kernel >= 256 pixels a slice, at most 16 slices; the
-// 128-tile kernel enough slices for ~2048 blocks (<= 64, >= 256 pixels a slice,
+// 128-tile kernel enough slices for <= 512 blocks (<= 64, >= 256 pixels a slice,
 // partials within part_cap)
 int64_t wgrad_kspan(const WgradArgs& a) {
     int64_t splits;
     if (wgrad_fast(a)) {
         const int64_t N = (int64_t)a.ks * a.ks * a.Ctot, MN = (int64_t)a.Cout * N;
         const int64_t tiles = ceil_div(N, 128) * ceil_div(a.Cout, 128);
-        // development: CFD_WGRAD_SMAX / CFD_WGRAD_TARGET (slices at most / block target)
+        // as many slices as fill whole rounds of resident blocks: 512 = two 64-KB-LDS
+        // blocks per CU, so a launch has no partial last round (576 blocks, 9 tiles
+        // x 64 slices, ran as two rounds, the second one eighth full).  Development:
+        // CFD_WGRAD_SMAX / CFD_WGRAD_TARGET (slices at most / blocks at most)
         static const int smax = getenv("CFD_WGRAD_SMAX") ? atoi(getenv("CFD_WGRAD_SMAX")) : 64;
-        static const int target = getenv("CFD_WGRAD_TARGET") ? atoi(getenv("CFD_WGRAD_TARGET")) : 2048;
-        splits = std::min<int64_t>({(int64_t)smax, ceil_div(target, tiles), ceil_div(a.P, 256),
+        static const int target = getenv("CFD_WGRAD_TARGET") ? atoi(getenv("CFD_WGRAD_TARGET")) : 512;
+        splits = std::min<int64_t>({(int64_t)smax, std::max<int64_t>(1, target / tiles), ceil_div(a.P, 256),
                                     std::max<int64_t>(1, a.part_cap / MN)});
         splits = std::max<int64_t>(1, splits);
         const int64_t span = ceil_div(a.P, splits);
