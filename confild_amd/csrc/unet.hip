@@ -807,22 +807,6 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         cfd::launch_colsum(dy, a.P, cout, 1, cpart, crow, st);
         cfd::launch_rows_accum(crow, 1, cout, GP(pre + ".bias"), st);
     };
-    auto gnp = [&](const Act& in, const float* ss, const float* stats, const std::string& pre, int silu,
-                   const float* dz) {
-        cfd::GnpArgs g{};
-        g.x1 = in.a;
-        g.x2 = in.b;
-        g.dz = dz;
-        g.ss = ss;
-        g.stats = stats;
-        g.part = gpp;
-        g.C1 = in.Ca;
-        g.C2 = in.Cb;
-        g.Ctot = in.C();
-        g.HW = in.H * in.W;
-        g.silu = silu;
-        cfd::launch_gn_param(g, B, GP(pre + ".weight"), GP(pre + ".bias"), st);
-    };
     if (pg) CFD_HIP(hipMemsetAsync(demb, 0, sizeof(float) * B * h->tdim, st));
 
     auto gfree = [&](const float* b1, const float* b2 = nullptr, const float* b3 = nullptr) -> float* {
@@ -863,8 +847,10 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         a.K = ks * ks * cin;
         cfd::launch_conv(a, plan_checked(a, kSplitCap), st);
     };
+    // with_param (training): the GroupNorm's parameter-gradient partials come out of
+    // the same statistics pass (GnbArgs::ppart) and are accumulated into dgamma / dbeta
     auto gnb = [&](const Act& in, const float* ss, const float* stats, const std::string& pre, int silu,
-                   const float* dz, const float* addsrc, float* out1, float* out2) {
+                   const float* dz, const float* addsrc, float* out1, float* out2, bool with_param = false) {
         cfd::GnbArgs g{};
         g.x1 = in.a;
         g.x2 = in.b;
@@ -882,7 +868,11 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         g.Ctot = in.C();
         g.HW = in.H * in.W;
         g.silu = silu;
+        if (with_param && pg) g.ppart = gpp;
         cfd::launch_gn_bwd(g, B, st);
+        if (g.ppart)
+            cfd::launch_gn_param_accum(gpp, B * cfd::gn_chunks(g.HW), g.Ctot, GP(pre + ".weight"), GP(pre + ".bias"),
+                                       st);
     };
 
     Act dcur;  // gradient w.r.t. the current activation (single contiguous tensor)
@@ -907,11 +897,8 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 a.tmode = 1;
                 cfd::launch_conv_in(a, st);
                 float* dh = gpool[1];
-                gnb(in, r.ss1, r.st1, "out.0", 1, G, nullptr, dh, nullptr);
-                if (pg) {
-                    wgrad(d_eps, c.out_channels, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, "out.2");
-                    gnp(in, r.ss1, r.st1, "out.0", 1, G);
-                }
+                gnb(in, r.ss1, r.st1, "out.0", 1, G, nullptr, dh, nullptr, true);
+                if (pg) wgrad(d_eps, c.out_channels, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, "out.2");
                 dcur = Act{dh, in.Ca, nullptr, 0, in.H, in.W};
                 break;
             }
@@ -945,9 +932,8 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 const Act h1{r.h1, rs.cout, nullptr, 0, in.H, in.W};
                 if (pg) wgrad(dout, rs.cout, h1, r.ss2, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".out_layers.3");
                 dconv(dout, rs.cout, in.H, in.W, rs.pre + ".out_layers.3.weight", rs.cout, in.H, in.W, 3, 1, 1, 0, G);
-                if (pg) gnp(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G);
                 float* dh1 = gfree(dout, G);
-                gnb(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr, dh1, nullptr);
+                gnb(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr, dh1, nullptr, true);
                 if (pg) {
                     wgrad(dh1, rs.cout, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".in_layers.2");
                     // emb_layers: d emb_out[b, c] = sum over pixels of dh1; its Linear(SiLU(emb))
@@ -969,10 +955,9 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                           0, sk);
                     addsrc = sk;
                 }
-                if (pg) gnp(in, r.ss1, r.st1, rs.pre + ".in_layers.0", 1, G);
                 float* dx = dh1;  // dh1 is consumed: reuse for the first source's gradient
                 gnb(in, r.ss1, r.st1, rs.pre + ".in_layers.0", 1, G, addsrc, dx,
-                    in.b ? dhs[r.skip_hs] : nullptr);
+                    in.b ? dhs[r.skip_hs] : nullptr, true);
                 dcur = Act{dx, in.Ca, nullptr, 0, in.H, in.W};
                 break;
             }
@@ -991,8 +976,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 if (pg) wgrad(dqkv, 3 * at.C, in, r.ss1, 0, in.H, in.W, 1, 1, 0, 0, at.pre + ".qkv");
                 float* dxn = gfree(dout, dA);
                 dconv(dqkv, 3 * at.C, in.H, in.W, at.pre + ".qkv.weight", at.C, in.H, in.W, 1, 1, 0, 0, dxn);
-                if (pg) gnp(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn);
-                gnb(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn, dout, dA, nullptr);
+                gnb(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn, dout, dA, nullptr, true);
                 dcur = Act{dA, at.C, nullptr, 0, in.H, in.W};
                 break;
             }

@@ -93,6 +93,9 @@ struct GnbArgs {
     int acc1, acc2;       // accumulate into out1 / out2 instead of overwriting
     double* part;         // scratch (B, nchunks, 32, 2)
     float* fin;           // scratch (B, 32, 2)
+    // optional (training): the GroupNorm parameter-gradient partials from the same
+    // pass, (B, nchunks, Ctot, 2) floats = (sum dz_eff xhat, sum dz_eff) per chunk
+    float* ppart;
     int C1, C2, Ctot, HW, silu, nchunks, B;
 };
 

@@ -526,65 +526,6 @@ __global__ __launch_bounds__(256) void rows_accum_kernel(const float* __restrict
     G[f] = G[f] + s;
 }
 
-// GroupNorm(+SiLU) parameter gradients, per (pixel chunk, sample): every thread
-// a channel quad of `rows` pixel rows; dz_eff = dy * SiLU'(z) (or dy), z = x sc +
-// sf (the forward's output before SiLU), xhat = (x - mean) rstd:
-// part[(b, chunk)][c] = (sum dz_eff xhat, sum dz_eff)
-__global__ __launch_bounds__(256) void gn_param_part_kernel(GnpArgs a) {
-    const int chunk = blockIdx.x;
-    const int64_t b = blockIdx.y;
-    const int Ctot = a.Ctot, cq = Ctot / 4, cpg = Ctot / 32;
-    const int HW = a.HW;
-    const int p0 = (int)((int64_t)HW * chunk / a.nchunks), p1 = (int)((int64_t)HW * (chunk + 1) / a.nchunks);
-    const int rows = 256 / cq;
-    const int q = threadIdx.x % cq, r0 = threadIdx.x / cq;
-    __shared__ float red[2][1024];
-    if (r0 < rows) {
-        const int c0 = 4 * q;
-        float sc[4], sf[4], mu[4], rs[4], g1[4] = {0.f, 0.f, 0.f, 0.f}, g2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = c0 + j, grp = c / cpg;
-            sc[j] = a.ss[(b * Ctot + c) * 2];
-            sf[j] = a.ss[(b * Ctot + c) * 2 + 1];
-            mu[j] = a.stats[(b * 32 + grp) * 2];
-            rs[j] = a.stats[(b * 32 + grp) * 2 + 1];
-        }
-        for (int p = p0 + r0; p < p1; p += rows) {
-            const int64_t pix = b * HW + p;
-            const f4 x = c0 < a.C1 ? *(const f4*)(a.x1 + pix * a.C1 + c0) : *(const f4*)(a.x2 + pix * a.C2 + (c0 - a.C1));
-            const f4 dy = *(const f4*)(a.dz + pix * Ctot + c0);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float d = dy[j];
-                if (a.silu) {
-                    const float z = x[j] * sc[j] + sf[j];
-                    const float s = sigm_t(z);
-                    d = d * (s * (1.0f + z * (1.0f - s)));
-                }
-                g1[j] += d * ((x[j] - mu[j]) * rs[j]);
-                g2[j] += d;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            red[0][r0 * Ctot + c0 + j] = g1[j];
-            red[1][r0 * Ctot + c0 + j] = g2[j];
-        }
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < Ctot; c += 256) {   // rows in order
-        float s1 = 0.f, s2 = 0.f;
-        for (int r = 0; r < rows; ++r) {
-            s1 += red[0][r * Ctot + c];
-            s2 += red[1][r * Ctot + c];
-        }
-        float* dst = a.part + ((b * a.nchunks + chunk) * (int64_t)Ctot + c) * 2;
-        dst[0] = s1;
-        dst[1] = s2;
-    }
-}
-
 // dgamma[c] += sum over (sample, chunk) of part, dbeta likewise: a block per 32
 // channels, 8 part lanes combined in order
 __global__ __launch_bounds__(256) void gn_param_accum_kernel(const float* __restrict__ part, int nparts, int Ctot,
@@ -827,18 +768,9 @@ void launch_rows_accum(const float* rows, int R, int64_t F, float* G, hipStream_
     check_launch("rows_accum_kernel");
 }
 
-int gn_param_chunks(int HW, int Ctot, int B) {   // ~256 blocks over the batch, >= 16 row passes a chunk
-    const int rows = std::max(1, 256 / (Ctot / 4));
-    const int64_t want = std::max<int64_t>(1, ceil_div(256, B));
-    return (int)std::min<int64_t>({kGnMaxChunks, want, std::max<int64_t>(1, ceil_div(HW, 16 * rows))});
-}
-
-void launch_gn_param(GnpArgs a, int B, float* dgamma, float* dbeta, hipStream_t st) {
-    a.nchunks = gn_param_chunks(a.HW, a.Ctot, B);
-    hipLaunchKernelGGL(gn_param_part_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
-    check_launch("gn_param_part_kernel");
-    hipLaunchKernelGGL(gn_param_accum_kernel, dim3((unsigned)ceil_div(a.Ctot, 32)), dim3(256), 0, st, a.part,
-                       a.nchunks * B, a.Ctot, dgamma, dbeta);
+void launch_gn_param_accum(const float* part, int nparts, int Ctot, float* dgamma, float* dbeta, hipStream_t st) {
+    hipLaunchKernelGGL(gn_param_accum_kernel, dim3((unsigned)ceil_div(Ctot, 32)), dim3(256), 0, st, part, nparts, Ctot,
+                       dgamma, dbeta);
     check_launch("gn_param_accum_kernel");
 }
 

@@ -23,16 +23,6 @@ struct WgradArgs {
     const unsigned* amax;
 };
 
-// GroupNorm(+SiLU) parameter gradient partials
-struct GnpArgs {
-    const float* x1;
-    const float* x2;
-    const float* dz;     // (B, HW, Ctot) gradient w.r.t. the GroupNorm(+SiLU) output
-    const float* ss;     // (B, Ctot, 2)
-    const float* stats;  // (B, 32, 2) mean / rstd
-    float* part;         // scratch: B * gn_param_chunks * Ctot * 2
-    int C1, C2, Ctot, HW, silu, nchunks;
-};
 
 // pixel slice of one block (P, Cout, Ctot, ks and part_cap of a set)
 int64_t wgrad_kspan(const WgradArgs& a);
@@ -44,8 +34,8 @@ size_t colsum_part_floats(int64_t n, int64_t F, int R);
 void launch_colsum(const float* X, int64_t n, int64_t F, int R, float* part, float* out, hipStream_t st);
 // G (F) += sum of the R rows of rows (R, F)
 void launch_rows_accum(const float* rows, int R, int64_t F, float* G, hipStream_t st);
-int gn_param_chunks(int HW, int Ctot, int B);
-void launch_gn_param(GnpArgs a, int B, float* dgamma, float* dbeta, hipStream_t st);
+// dgamma / dbeta += the (nparts, Ctot, 2) partials in part order (gn_bwd_partial's PP form)
+void launch_gn_param_accum(const float* part, int nparts, int Ctot, float* dgamma, float* dbeta, hipStream_t st);
 void launch_linear_wgrad(const float* d, const float* a, int B, int K, int N, int act, float* GW, float* Gb,
                          hipStream_t st);
 void launch_linear_dgrad(const float* d, const float* W, const float* x, int B, int K, int N, int act, int accumulate,

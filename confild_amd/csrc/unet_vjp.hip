@@ -44,23 +44,34 @@ __device__ __forceinline__ GnbQuad gnb_quad(const GnbArgs& a, int64_t b, int c0)
     return k;
 }
 
-// g = gamma * dz * SiLU'(z) (or gamma * dz), xhat = (x - mean) * rstd, for 4 channels
-__device__ __forceinline__ void gnb_load(const GnbArgs& a, const GnbQuad& k, int64_t pix, int c0, f4& g, f4& xh) {
+// dz_eff = dz * SiLU'(z) (or dz), g = gamma * dz_eff, xhat = (x - mean) * rstd, for 4 channels
+__device__ __forceinline__ void gnb_load_d(const GnbArgs& a, const GnbQuad& k, int64_t pix, int c0, f4& d, f4& xh) {
     const f4 x = c0 < a.C1 ? *(const f4*)(a.x1 + pix * a.C1 + c0) : *(const f4*)(a.x2 + pix * a.C2 + (c0 - a.C1));
-    f4 dz = *(const f4*)(a.dz + pix * a.Ctot + c0);
+    const f4 dz = *(const f4*)(a.dz + pix * a.Ctot + c0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        float d = dz[j];
+        float dj = dz[j];
         if (a.silu) {
             const float z = x[j] * k.sc[j] + k.sh[j];
             const float sg = sigmoid_f(z);
-            d = d * (sg * (1.0f + z * (1.0f - sg)));
+            dj = dj * (sg * (1.0f + z * (1.0f - sg)));
         }
-        g[j] = d * k.gm[j];
+        d[j] = dj;
         xh[j] = (x[j] - k.mean[j]) * k.rstd[j];
     }
 }
+__device__ __forceinline__ void gnb_load(const GnbArgs& a, const GnbQuad& k, int64_t pix, int c0, f4& g, f4& xh) {
+    f4 d;
+    gnb_load_d(a, k, pix, c0, d, xh);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = d[j] * k.gm[j];
+}
 
+// PP (training): the per-channel sums are of dz_eff, not g = gamma dz_eff, so the
+// same pass also yields the parameter-gradient partials (sum dz_eff xhat, sum
+// dz_eff) per (chunk, channel) -- gn_param_part's pass over the same data folded
+// in; the group sums are then sum_c gamma_c (per-channel sum), in float64
+template <bool PP>
 __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnbArgs a) {
     const int chunk = blockIdx.x;
     const int64_t b = blockIdx.y;
@@ -76,7 +87,10 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnbArgs a) {
         const GnbQuad k = gnb_quad(a, b, c0);
         for (int p = p0 + r0; p < p1; p += rows) {
             f4 g, xh;
-            gnb_load(a, k, b * HW + p, c0, g, xh);
+            if constexpr (PP)
+                gnb_load_d(a, k, b * HW + p, c0, g, xh);
+            else
+                gnb_load(a, k, b * HW + p, c0, g, xh);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 s[j] += g[j];
@@ -95,12 +109,30 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnbArgs a) {
         double ts = 0, ts2 = 0;
         for (int r = 0; r < rows; ++r)
             for (int c = grp * cpg; c < (grp + 1) * cpg; ++c) {
-                ts += red[0][r * Ctot + c];
-                ts2 += red[1][r * Ctot + c];
+                if constexpr (PP) {
+                    const double gm = (double)a.gamma[c];
+                    ts += gm * red[0][r * Ctot + c];
+                    ts2 += gm * red[1][r * Ctot + c];
+                } else {
+                    ts += red[0][r * Ctot + c];
+                    ts2 += red[1][r * Ctot + c];
+                }
             }
         double* dst = a.part + ((b * a.nchunks + chunk) * 32 + grp) * 2;
         dst[0] = ts;
         dst[1] = ts2;
+    }
+    if constexpr (PP) {   // rows in order, per channel: (sum dz_eff xhat, sum dz_eff)
+        for (int c = threadIdx.x; c < Ctot; c += 256) {
+            double t1 = 0, t2 = 0;
+            for (int r = 0; r < rows; ++r) {
+                t1 += red[1][r * Ctot + c];
+                t2 += red[0][r * Ctot + c];
+            }
+            float* dst = a.ppart + ((b * a.nchunks + chunk) * (int64_t)Ctot + c) * 2;
+            dst[0] = (float)t1;
+            dst[1] = (float)t2;
+        }
     }
 }
 
@@ -367,7 +399,10 @@ void launch_gn_bwd(const GnbArgs& a0, int B, hipStream_t st) {
     GnbArgs a = a0;
     a.nchunks = gn_chunks(a.HW);
     a.B = B;
-    hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
+    if (a.ppart)
+        hipLaunchKernelGGL(gn_bwd_partial_kernel<true>, dim3(a.nchunks, B), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(gn_bwd_partial_kernel<false>, dim3(a.nchunks, B), dim3(256), 0, st, a);
     check_launch("gn_bwd_partial_kernel");
     hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B), dim3(1024), 0, st, a);
     check_launch("gn_bwd_finalize_kernel");
