@@ -437,6 +437,82 @@ __global__ __launch_bounds__(256) void gn_act_kernel(WgradArgs a, int64_t nquads
     }
 }
 
+// Thin layers (the U-Net's 1-channel input and output convolutions: Ctot or
+// Cout <= 4, 3x3 stride 1): the 64x64 tiles would be 1/16 to 1/64 occupied, so
+// one thread per channel of the wide side instead, the narrow side's <= 4 x 9
+// sums in registers.  WIDE_OUT (input conv, Cout wide): threads walk the slice's
+// output pixels, dY read once and coalesced, the 9 taps' narrow inputs
+// broadcast.  Otherwise (output conv, Ctot wide): threads walk the slice's INPUT
+// pixels, X read once and coalesced, the <= 4 dY values of the up-to-9 output
+// pixels each input pixel feeds broadcast.  Each thread sums its slice in pixel
+// order; the slices are combined in order by wgrad_accum_kernel (deterministic).
+template <bool WIDE_OUT, int NN>
+__global__ __launch_bounds__(64) void conv_wgrad_thin_kernel(WgradArgs a) {
+    const int w = blockIdx.x * 64 + threadIdx.x;               // wide-side channel
+    const int wide = WIDE_OUT ? a.Cout : a.Ctot, narrow = WIDE_OUT ? a.Ctot : a.Cout;
+    const int ks = a.ks, taps = ks * ks;
+    const int N = taps * a.Ctot;
+    const int64_t MN = (int64_t)a.Cout * N;
+    const int64_t kbeg = (int64_t)blockIdx.z * a.kspan, kend = min(a.P, kbeg + a.kspan);
+    const int H = a.Hout, W = a.Wout, HW = H * W;   // stride 1, no upsample: input = output geometry
+    float acc[NN][9];
+#pragma unroll
+    for (int n = 0; n < NN; ++n)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[n][t] = 0.f;
+    auto xval = [&](int64_t pix, int64_t b, int ci) -> float {   // the forward input (GroupNorm affine / SiLU)
+        float v = ci < a.C1 ? a.src1[pix * a.C1 + ci] : a.src2[pix * a.C2 + (ci - a.C1)];
+        if (a.ss) {
+            const float* s = a.ss + (b * a.Ctot + ci) * 2;
+            v = v * s[0] + s[1];
+            if (a.silu) v = silu_f(v);
+        }
+        return v;
+    };
+    if (w < wide) {
+        for (int64_t k = kbeg; k < kend; ++k) {   // k: output pixel (WIDE_OUT) or input pixel
+            const int64_t b = k / HW;
+            const int rem = (int)(k - b * HW), y = rem / W, x = rem - y * W;
+            if constexpr (WIDE_OUT) {
+                const float d = a.dy[k * a.Cout + w];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    if (t >= taps) continue;
+                    const int ty = t / ks, tx = t - ty * ks;
+                    const int iy = y - a.pad + ty, ix = x - a.pad + tx;
+                    if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+                    const int64_t pix = (b * H + iy) * W + ix;
+#pragma unroll
+                    for (int n = 0; n < NN; ++n)
+                        if (n < narrow) acc[n][t] = fmaf(d, xval(pix, b, n), acc[n][t]);
+                }
+            } else {
+                const float xv = xval(k, b, w);
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    if (t >= taps) continue;
+                    const int ty = t / ks, tx = t - ty * ks;
+                    const int oy = y + a.pad - ty, ox = x + a.pad - tx;   // the output pixel this tap of k feeds
+                    if (oy < 0 || oy >= H || ox < 0 || ox >= W) continue;
+                    const int64_t op = (b * H + oy) * W + ox;
+#pragma unroll
+                    for (int n = 0; n < NN; ++n)
+                        if (n < narrow) acc[n][t] = fmaf(a.dy[op * a.Cout + n], xv, acc[n][t]);
+                }
+            }
+        }
+        float* part = a.part + (int64_t)blockIdx.z * MN;
+#pragma unroll
+        for (int n = 0; n < NN; ++n)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                if (n >= narrow || t >= taps) continue;
+                const int co = WIDE_OUT ? w : n, ci = WIDE_OUT ? n : w;
+                part[(int64_t)co * N + t * a.Ctot + ci] = acc[n][t];
+            }
+    }
+}
+
 // G[co][ci][tap] (the reference weight layout) += sum_z part[z][co][tap * Ctot + ci]
 __global__ __launch_bounds__(256) void wgrad_accum_kernel(const float* __restrict__ part, int Cout, int Ctot, int taps,
                                                           int splits, float* __restrict__ G) {
@@ -646,6 +722,12 @@ namespace {
 bool wgrad_fast(const WgradArgs& a) {
     return a.Ctot % 128 == 0 && a.Cout % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0;
 }
+// conv_wgrad_thin_kernel's shapes (CFD_WGRAD_THIN=0: the 64-tile kernel)
+bool wgrad_thin(const WgradArgs& a) {
+    static const int on = getenv("CFD_WGRAD_THIN") ? atoi(getenv("CFD_WGRAD_THIN")) : 1;
+    return on && !wgrad_fast(a) && (a.Ctot <= 4 || a.Cout <= 4) && a.stride == 1 && !a.up && a.ks <= 3 &&
+           a.Hin == a.Hout && a.Win == a.Wout;
+}
 }  // namespace
 
 // pixel slices: the 64-tile kernel >= 256 pixels a slice, at most 16 slices; the
@@ -668,8 +750,14 @@ int64_t wgrad_kspan(const WgradArgs& a) {
         const int64_t span = ceil_div(a.P, splits);
         return (span + 31) / 32 * 32;
     }
-    // 64-tile kernel (thin layers: the 1-channel input / output convolutions, narrow
-    // test topologies): ~1024 blocks, <= 128 slices of >= 256 pixels
+    if (wgrad_thin(a)) {   // ~1024 blocks of 64 wide-side channels, slices of >= 256 pixels
+        const int64_t MN = (int64_t)a.Cout * a.ks * a.ks * a.Ctot;
+        const int64_t blocks = ceil_div(a.Ctot <= 4 ? a.Cout : a.Ctot, 64);
+        splits = std::min<int64_t>({ceil_div(1024, blocks), ceil_div(a.P, 256), std::max<int64_t>(1, a.part_cap / MN)});
+        splits = std::max<int64_t>(1, splits);
+        return ceil_div(a.P, splits);
+    }
+    // 64-tile kernel (narrow test topologies): ~1024 blocks, <= 128 slices of >= 256 pixels
     const int64_t N = (int64_t)a.ks * a.ks * a.Ctot, MN = (int64_t)a.Cout * N;
     const int64_t tiles = ceil_div(N, 64) * ceil_div(a.Cout, 64);
     splits = std::min<int64_t>({128, ceil_div(1024, tiles), ceil_div(a.P, 256), std::max<int64_t>(1, a.part_cap / MN)});
@@ -730,6 +818,18 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
             hipLaunchKernelGGL(conv_wgrad128_kernel, grid, dim3(256), 0, st, b, act);
             check_launch("conv_wgrad128_kernel");
         }
+    } else if (wgrad_thin(a)) {
+        const bool wide_out = a.Ctot <= 4;
+        const int narrow = wide_out ? a.Ctot : a.Cout;
+        const dim3 grid((unsigned)ceil_div(wide_out ? a.Cout : a.Ctot, 64), 1, (unsigned)splits);
+        if (wide_out) {
+            if (narrow == 1) hipLaunchKernelGGL((conv_wgrad_thin_kernel<true, 1>), grid, dim3(64), 0, st, a);
+            else hipLaunchKernelGGL((conv_wgrad_thin_kernel<true, 4>), grid, dim3(64), 0, st, a);
+        } else {
+            if (narrow == 1) hipLaunchKernelGGL((conv_wgrad_thin_kernel<false, 1>), grid, dim3(64), 0, st, a);
+            else hipLaunchKernelGGL((conv_wgrad_thin_kernel<false, 4>), grid, dim3(64), 0, st, a);
+        }
+        check_launch("conv_wgrad_thin_kernel");
     } else {
         const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(a.Cout, 64), (unsigned)splits);
         hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, a);
