@@ -1,0 +1,12 @@
+# which of the two TrainLoop changes moved the step: thin weight gradients on / off vs the previous library
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r04t; mkdir -p $O
+for r in 1 2; do
+for spec in "libconfild_hip_prev.so 1" "libconfild_hip.so 1" "libconfild_hip.so 0"; do
+set -- $spec
+CFD_LIB=$1 CFD_WGRAD_THIN=$2 timeout -k 10 300 python3 tools/kbench.py utrain --batch 16 --size 128 > $O/ut.out 2> $O/ut.err || { tail -20 $O/ut.err; exit 4; }
+echo "$1 THIN=$2 $(grep unet_train_step $O/ut.out | cut -c60-260)"
+done; done
+CFD_WGRAD_THIN=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ut -o run -- python3 tools/kbench.py utrain --batch 16 --size 128 > $O/utp.out 2> $O/utp.err || { tail -20 $O/utp.err; exit 5; }
+rm -f $O/ut/run_kernel_trace.csv
