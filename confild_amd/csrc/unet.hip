@@ -869,10 +869,9 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         g.HW = in.H * in.W;
         g.silu = silu;
         if (with_param && pg) g.ppart = gpp;
-        cfd::launch_gn_bwd(g, B, st);
+        const int nch = cfd::launch_gn_bwd(g, B, st);
         if (g.ppart)
-            cfd::launch_gn_param_accum(gpp, B * cfd::gn_chunks(g.HW), g.Ctot, GP(pre + ".weight"), GP(pre + ".bias"),
-                                       st);
+            cfd::launch_gn_param_accum(gpp, B * nch, g.Ctot, GP(pre + ".weight"), GP(pre + ".bias"), st);
     };
 
     Act dcur;  // gradient w.r.t. the current activation (single contiguous tensor)

@@ -172,7 +172,7 @@ void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t s
 size_t attention_split_floats(int T, int C);
 void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st);
 // backward (unet_vjp.hip)
-void launch_gn_bwd(const GnbArgs& a, int B, hipStream_t st);
+int launch_gn_bwd(const GnbArgs& a, int B, hipStream_t st);   // returns the pixel chunks used
 void launch_attention_bwd(const AttnBwdArgs& a, int CH, int heads, int B, hipStream_t st);
 void launch_add(float* y, const float* x, int64_t n, hipStream_t st);
 void launch_temb(const int64_t* t, const float* freqs, float* out, int dim, int B, hipStream_t st);

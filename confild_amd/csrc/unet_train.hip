@@ -438,17 +438,19 @@ __global__ __launch_bounds__(256) void gn_act_kernel(WgradArgs a, int64_t nquads
 }
 
 // Thin layers (the U-Net's 1-channel input and output convolutions: Ctot or
-// Cout <= 4, 3x3 stride 1): the 64x64 tiles would be 1/16 to 1/64 occupied, so
-// one thread per channel of the wide side instead, the narrow side's <= 4 x 9
-// sums in registers.  WIDE_OUT (input conv, Cout wide): threads walk the slice's
-// output pixels, dY read once and coalesced, the 9 taps' narrow inputs
-// broadcast.  Otherwise (output conv, Ctot wide): threads walk the slice's INPUT
-// pixels, X read once and coalesced, the <= 4 dY values of the up-to-9 output
-// pixels each input pixel feeds broadcast.  Each thread sums its slice in pixel
-// order; the slices are combined in order by wgrad_accum_kernel (deterministic).
+// Cout <= 4, 3x3 stride 1): the 64x64 tiles would be 1/16 to 1/64 occupied.
+// Here a workgroup is 64 channels of the wide side x 16 pixel lanes; a thread
+// keeps the narrow side's <= 4 x 9 sums in registers and walks every 16th pixel
+// of the slice, four pixels' loads issued before their FMAs.  WIDE_OUT (input
+// conv, Cout wide): the pixels are output pixels, dY read once and coalesced, the
+// taps' narrow inputs broadcast.  Otherwise (output conv, Ctot wide): the pixels
+// are INPUT pixels, X read once and coalesced, the <= 4 dY values of the output
+// pixels each feeds broadcast.  The 16 lanes' sums are added in lane order, the
+// slices by wgrad_accum_kernel in slice order (deterministic).
 template <bool WIDE_OUT, int NN>
-__global__ __launch_bounds__(64) void conv_wgrad_thin_kernel(WgradArgs a) {
-    const int w = blockIdx.x * 64 + threadIdx.x;               // wide-side channel
+__global__ __launch_bounds__(1024) void conv_wgrad_thin_kernel(WgradArgs a) {
+    constexpr int NPL = 16, U = NN == 1 ? 4 : 1;   // U: pixels whose loads are in flight together
+    const int w = blockIdx.x * 64 + (threadIdx.x & 63), pl = threadIdx.x >> 6;   // wide channel, pixel lane
     const int wide = WIDE_OUT ? a.Cout : a.Ctot, narrow = WIDE_OUT ? a.Ctot : a.Cout;
     const int ks = a.ks, taps = ks * ks;
     const int N = taps * a.Ctot;
@@ -469,46 +471,55 @@ __global__ __launch_bounds__(64) void conv_wgrad_thin_kernel(WgradArgs a) {
         }
         return v;
     };
-    if (w < wide) {
-        for (int64_t k = kbeg; k < kend; ++k) {   // k: output pixel (WIDE_OUT) or input pixel
-            const int64_t b = k / HW;
+    const bool on = w < wide;
+    for (int64_t k0 = kbeg + pl; k0 < kend; k0 += NPL * U) {
+        float wv[U];                 // the wide-side value of each pixel (dY or X)
+        float nv[U][NN][9];          // the narrow-side value of each (pixel, narrow index, tap), 0 off-image
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = k0 + (int64_t)u * NPL;
+            const bool kin = on && k < kend;
+            const int64_t b = kin ? k / HW : 0;
             const int rem = (int)(k - b * HW), y = rem / W, x = rem - y * W;
-            if constexpr (WIDE_OUT) {
-                const float d = a.dy[k * a.Cout + w];
+            wv[u] = 0.f;
+            if (kin) wv[u] = WIDE_OUT ? a.dy[k * a.Cout + w] : xval(k, b, w);
 #pragma unroll
-                for (int t = 0; t < 9; ++t) {
-                    if (t >= taps) continue;
-                    const int ty = t / ks, tx = t - ty * ks;
-                    const int iy = y - a.pad + ty, ix = x - a.pad + tx;
-                    if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
-                    const int64_t pix = (b * H + iy) * W + ix;
+            for (int t = 0; t < 9; ++t) {
+                const int ty = t / 3, tx = t - 3 * ty;   // ks == 3 (ks == 1: t == 0 only, tap (0, 0))
+                const int dy_ = ks == 3 ? ty - a.pad : 0, dx_ = ks == 3 ? tx - a.pad : 0;
+                const int yy = WIDE_OUT ? y + dy_ : y - dy_, xx = WIDE_OUT ? x + dx_ : x - dx_;
+                const bool ok = kin && t < taps && yy >= 0 && yy < H && xx >= 0 && xx < W;
+                const int64_t q = (b * H + yy) * W + xx;
 #pragma unroll
-                    for (int n = 0; n < NN; ++n)
-                        if (n < narrow) acc[n][t] = fmaf(d, xval(pix, b, n), acc[n][t]);
-                }
-            } else {
-                const float xv = xval(k, b, w);
-#pragma unroll
-                for (int t = 0; t < 9; ++t) {
-                    if (t >= taps) continue;
-                    const int ty = t / ks, tx = t - ty * ks;
-                    const int oy = y + a.pad - ty, ox = x + a.pad - tx;   // the output pixel this tap of k feeds
-                    if (oy < 0 || oy >= H || ox < 0 || ox >= W) continue;
-                    const int64_t op = (b * H + oy) * W + ox;
-#pragma unroll
-                    for (int n = 0; n < NN; ++n)
-                        if (n < narrow) acc[n][t] = fmaf(a.dy[op * a.Cout + n], xv, acc[n][t]);
-                }
+                for (int n = 0; n < NN; ++n)
+                    nv[u][n][t] = ok && n < narrow ? (WIDE_OUT ? xval(q, b, n) : a.dy[q * a.Cout + n]) : 0.f;
             }
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int n = 0; n < NN; ++n)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[n][t] = fmaf(wv[u], nv[u][n][t], acc[n][t]);
+    }
+    // the 16 pixel lanes' sums, added in lane order
+    __shared__ float red[NPL][64][NN * 9];
+#pragma unroll
+    for (int n = 0; n < NN; ++n)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) red[pl][threadIdx.x & 63][n * 9 + t] = acc[n][t];
+    __syncthreads();
+    if (pl == 0 && on) {
         float* part = a.part + (int64_t)blockIdx.z * MN;
 #pragma unroll
         for (int n = 0; n < NN; ++n)
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
                 if (n >= narrow || t >= taps) continue;
+                float v = red[0][threadIdx.x][n * 9 + t];
+                for (int l = 1; l < NPL; ++l) v += red[l][threadIdx.x][n * 9 + t];
                 const int co = WIDE_OUT ? w : n, ci = WIDE_OUT ? n : w;
-                part[(int64_t)co * N + t * a.Ctot + ci] = acc[n][t];
+                part[(int64_t)co * N + t * a.Ctot + ci] = v;
             }
     }
 }
@@ -750,10 +761,10 @@ int64_t wgrad_kspan(const WgradArgs& a) {
         const int64_t span = ceil_div(a.P, splits);
         return (span + 31) / 32 * 32;
     }
-    if (wgrad_thin(a)) {   // ~1024 blocks of 64 wide-side channels, slices of >= 256 pixels
+    if (wgrad_thin(a)) {   // ~512 blocks of 64 wide-side channels x 16 pixel lanes, slices of >= 512 pixels
         const int64_t MN = (int64_t)a.Cout * a.ks * a.ks * a.Ctot;
         const int64_t blocks = ceil_div(a.Ctot <= 4 ? a.Cout : a.Ctot, 64);
-        splits = std::min<int64_t>({ceil_div(1024, blocks), ceil_div(a.P, 256), std::max<int64_t>(1, a.part_cap / MN)});
+        splits = std::min<int64_t>({ceil_div(512, blocks), ceil_div(a.P, 512), std::max<int64_t>(1, a.part_cap / MN)});
         splits = std::max<int64_t>(1, splits);
         return ceil_div(a.P, splits);
     }
@@ -823,11 +834,11 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
         const int narrow = wide_out ? a.Ctot : a.Cout;
         const dim3 grid((unsigned)ceil_div(wide_out ? a.Cout : a.Ctot, 64), 1, (unsigned)splits);
         if (wide_out) {
-            if (narrow == 1) hipLaunchKernelGGL((conv_wgrad_thin_kernel<true, 1>), grid, dim3(64), 0, st, a);
-            else hipLaunchKernelGGL((conv_wgrad_thin_kernel<true, 4>), grid, dim3(64), 0, st, a);
+            if (narrow == 1) hipLaunchKernelGGL((conv_wgrad_thin_kernel<true, 1>), grid, dim3(1024), 0, st, a);
+            else hipLaunchKernelGGL((conv_wgrad_thin_kernel<true, 4>), grid, dim3(1024), 0, st, a);
         } else {
-            if (narrow == 1) hipLaunchKernelGGL((conv_wgrad_thin_kernel<false, 1>), grid, dim3(64), 0, st, a);
-            else hipLaunchKernelGGL((conv_wgrad_thin_kernel<false, 4>), grid, dim3(64), 0, st, a);
+            if (narrow == 1) hipLaunchKernelGGL((conv_wgrad_thin_kernel<false, 1>), grid, dim3(1024), 0, st, a);
+            else hipLaunchKernelGGL((conv_wgrad_thin_kernel<false, 4>), grid, dim3(1024), 0, st, a);
         }
         check_launch("conv_wgrad_thin_kernel");
     } else {

@@ -392,12 +392,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-void launch_gn_bwd(const GnbArgs& a0, int B, hipStream_t st) {
+int launch_gn_bwd(const GnbArgs& a0, int B, hipStream_t st) {
     CFD_REQUIRE(a0.Ctot % 32 == 0 && a0.C1 % 4 == 0 && a0.C2 % 4 == 0 && a0.Ctot <= 1024, CFD_ESHAPE,
                 "GroupNorm32 backward needs channels % 32 == 0 (<= 1024)");
     CFD_REQUIRE(a0.C2 == 0 || a0.out2, CFD_ESTATE, "GroupNorm backward: second-source gradient needs out2");
     GnbArgs a = a0;
-    a.nchunks = gn_chunks(a.HW);
+    // with parameter partials (training) ~256 blocks over the batch, >= 16 row passes
+    // a chunk: the (B x chunks) partials are then few enough for one accumulation
+    // block per 32 channels (4096 partial rows at 128^2 took 51 us to accumulate)
+    if (a.ppart) {
+        const int rows = std::max(1, 256 / (a.Ctot / 4));
+        a.nchunks = (int)std::min<int64_t>({kGnMaxChunks, std::max<int64_t>(1, ceil_div(256, B)),
+                                            std::max<int64_t>(1, ceil_div(a.HW, 16 * rows))});
+    } else {
+        a.nchunks = gn_chunks(a.HW);
+    }
     a.B = B;
     if (a.ppart)
         hipLaunchKernelGGL(gn_bwd_partial_kernel<true>, dim3(a.nchunks, B), dim3(256), 0, st, a);
@@ -409,6 +418,7 @@ void launch_gn_bwd(const GnbArgs& a0, int B, hipStream_t st) {
     const int64_t nq = ceil_div((int64_t)B * a.HW, GNB_PIX) * (a.Ctot / 4);
     hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a);
     check_launch("gn_bwd_apply_kernel");
+    return a.nchunks;
 }
 
 template <int CH>
