@@ -282,6 +282,11 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
     if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
 
+// UP: the forward input was nearest-2x upsampled.  The block's 128 columns lie in
+// one source (launch_conv_wgrad: act, or C1 % 128 == 0), chosen once per block;
+// a thread's 4 pixels of a step are consecutive, decoded once and stepped; 32-bit
+// element offsets (launch_conv_wgrad checks P * Cout and the sources' sizes).
+template <bool UP>
 __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, const float* __restrict__ act) {
     constexpr int T = 128, KS = 32;
     constexpr int PLANE = T * KS * 2;   // bytes of one f16 [128][32] plane
@@ -293,42 +298,48 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
     const int tap = n0 / a.Ctot, ci0 = n0 - tap * a.Ctot;
     const int ty = tap / a.ks, tx = tap - ty * a.ks;
     const int kbeg = (int)(blockIdx.z * a.kspan), kend = (int)min(a.P, (int64_t)kbeg + a.kspan);   // P < 2^31
-    const int HWo = a.Hout * a.Wout;
+    const int HWo = a.Hout * a.Wout, Wo = a.Wout, Ho = a.Hout;
     const float sy = wg_scale(a.amax[0]), sx = wg_scale(a.amax[1]);
     const int q = tid >> 3, ko = tid & 7;   // rows 4q..4q+3 (both operands), pixels 4ko..4ko+3 of a step
-    const float rhw = 1.0f / (float)HWo, rw = 1.0f / (float)a.Wout;   // fdiv24: P < 2^24 (launch_conv_wgrad)
+    const float rhw = 1.0f / (float)HWo, rw = 1.0f / (float)Wo;   // fdiv24: P < 2^24 (launch_conv_wgrad)
+    // this block's X columns: one source, its row stride and channel offset
+    const float* xs;
+    int xld, xc;
+    if (act) {
+        xs = act, xld = a.Ctot, xc = ci0;
+    } else if (ci0 < a.C1) {
+        xs = a.src1, xld = a.C1, xc = ci0;
+    } else {
+        xs = a.src2, xld = a.C2, xc = ci0 - a.C1;
+    }
+    xs += xc + 4 * q;
+    const bool yrow = m0 + 4 * q < M;
+    const float* ys = a.dy + m0 + 4 * q;
+    const int iyo = UP ? ty - a.pad : ty - a.pad, ixo = UP ? tx - a.pad : tx - a.pad;
+    const int Hlim = UP ? 2 * a.Hin : a.Hin, Wlim = UP ? 2 * a.Win : a.Win;
     f4 yv[4], xv[4];   // [pixel]: 4 rows each
     auto load = [&](int k0) {
+        const int kb = k0 + 4 * ko;          // the thread's first pixel; the next 3 follow it
+        int b = fdiv24(kb, HWo, rhw);
+        const int rem = kb - b * HWo;
+        int oy = fdiv24(rem, Wo, rw), ox = rem - oy * Wo;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const int k = k0 + 4 * ko + p;
+            const int k = kb + p;
+            if (p > 0) {                      // step to the next output pixel
+                if (++ox == Wo) {
+                    ox = 0;
+                    if (++oy == Ho) oy = 0, ++b;
+                }
+            }
             f4 y = f4{0.f, 0.f, 0.f, 0.f}, x = f4{0.f, 0.f, 0.f, 0.f};
             if (k < kend) {
-                if (m0 + 4 * q < M) y = *(const f4*)(a.dy + (int64_t)k * M + m0 + 4 * q);
-                const int b = fdiv24(k, HWo, rhw);
-                const int rem = k - b * HWo;
-                const int oy = fdiv24(rem, a.Wout, rw), ox = rem - oy * a.Wout;
-                int iy, ix;
-                bool ok;
-                if (a.up) {
-                    iy = oy - a.pad + ty;
-                    ix = ox - a.pad + tx;
-                    ok = iy >= 0 && iy < 2 * a.Hin && ix >= 0 && ix < 2 * a.Win;
-                    iy >>= 1;
-                    ix >>= 1;
-                } else {
-                    iy = oy * a.stride - a.pad + ty;
-                    ix = ox * a.stride - a.pad + tx;
-                    ok = iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-                }
-                if (ok) {
-                    const int64_t pix = ((int64_t)b * a.Hin + iy) * a.Win + ix;
-                    const int ci = ci0 + 4 * q;
-                    if (act)
-                        x = *(const f4*)(act + pix * a.Ctot + ci);
-                    else
-                        x = ci < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + ci)
-                                      : *(const f4*)(a.src2 + pix * a.C2 + (ci - a.C1));
+                if (yrow) y = *(const f4*)(ys + (unsigned)k * (unsigned)M);
+                int iy = UP ? oy + iyo : oy * a.stride + iyo, ix = UP ? ox + ixo : ox * a.stride + ixo;
+                if (iy >= 0 && iy < Hlim && ix >= 0 && ix < Wlim) {
+                    if (UP) iy >>= 1, ix >>= 1;
+                    const unsigned pix = ((unsigned)b * a.Hin + iy) * a.Win + ix;
+                    x = *(const f4*)(xs + pix * (unsigned)xld);
                 }
             }
             yv[p] = y;
@@ -791,7 +802,10 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
         CFD_REQUIRE(a.P < (int64_t)1 << 31, CFD_ESHAPE, "weight gradient over 2^31 or more pixels");
         // split-f16 products (CFD_WGRAD_SPLIT=0: the exact fp32-MFMA kernel)
         static const int split_env = getenv("CFD_WGRAD_SPLIT") ? atoi(getenv("CFD_WGRAD_SPLIT")) : 1;
-        const bool split = split_env && a.amax_out && a.P < (1 << 24);   // fdiv24 pixel decode
+        // fdiv24 pixel decode; 32-bit element offsets; one source per 128-column tile
+        const int64_t srows0 = (int64_t)(a.P / ((int64_t)a.Hout * a.Wout)) * a.Hin * a.Win;
+        const bool split = split_env && a.amax_out && a.P < (1 << 24) && a.P * a.Cout < (1ll << 31) &&
+                           srows0 * a.Ctot < (1ll << 31) && (a.ss || a.C2 == 0 || a.C1 % 128 == 0);
         unsigned* amax = a.amax_out;
         auto absmax = [&](const float* x, int64_t n, unsigned* out) {
             const int64_t n4 = n / 4;
@@ -823,7 +837,10 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
         }
         const dim3 grid((unsigned)(N / 128), (unsigned)ceil_div(a.Cout, 128), (unsigned)splits);
         if (split) {
-            hipLaunchKernelGGL(conv_wgrad128_split_kernel, grid, dim3(256), 0, st, b, act);
+            if (a.up)
+                hipLaunchKernelGGL(conv_wgrad128_split_kernel<true>, grid, dim3(256), 0, st, b, act);
+            else
+                hipLaunchKernelGGL(conv_wgrad128_split_kernel<false>, grid, dim3(256), 0, st, b, act);
             check_launch("conv_wgrad128_split_kernel");
         } else {
             hipLaunchKernelGGL(conv_wgrad128_kernel, grid, dim3(256), 0, st, b, act);
