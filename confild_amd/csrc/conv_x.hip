@@ -401,6 +401,15 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     // unpadded); the pad columns load as zeros and are never read
     constexpr int HW2 = TW < 32 ? (TW + 2 + 3) / 4 * 4 : TW + 2;
     constexpr int TR = BM / TW, NPX = (TR + 2) * HW2;
+    // halo LDS offset of 16-B chunk `chunk` of halo pixel px in halo row hr: the
+    // xswz swizzle, and at TW = 16 (a 32-pixel fragment block spans two halo rows
+    // 20 pixels apart) the chunk rotation also takes the row, (px/4 + 3 hr) mod 4, so
+    // that the two rows' pixels of one ds_read_b128 lane group fall in different
+    // bank slots (PMC: 0.24 LDS bank-conflict rate with xswz alone)
+    auto hswz = [](int px, int hr, int chunk) {
+        if constexpr (TW == 16) return px * 64 + ((chunk ^ (((px >> 2) + 3 * hr) & 3)) << 4);
+        else return xswz(px, chunk);
+    };
     constexpr int HPLANE = NPX * 64;                  // one f16 plane of the halo (64 B per pixel)
     constexpr int HIT = (NPX * 8 + NTG - 1) / NTG;    // 16-B halo pieces per thread
     constexpr int BPLANE = BN * 64, BSTAGE = PL * BPLANE;
@@ -508,7 +517,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
         for (int it = 0; it < HIT; ++it) {
             const int e = gt + it * NTG;
             if (e < NPX * 8) {
-                const int off = xswz(e >> 3, kq >> 1) + (kq & 1) * 8;
+                const int off = hswz(e >> 3, (e >> 3) / HW2, kq >> 1) + (kq & 1) * 8;
                 if constexpr (SB) {   // already bf16: the 8 loaded bytes as they are
                     *(uint2*)(halo + off) = rh[it];
                 } else if constexpr (BF) {
@@ -553,11 +562,12 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
     const int l32 = lane & 31, hsel = lane >> 5;
-    int hb[2];   // halo pixel of tap (0, 0) for this lane's output pixel, per 32-row block
+    int hb[2], hrb[2];   // halo pixel and halo row of tap (0, 0) for this lane's output pixel, per 32-row block
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int p = wm * 64 + 32 * i + l32;
         hb[i] = (p / TW) * HW2 + (p % TW);
+        hrb[i] = p / TW;
     }
     const int brow0 = wn * 64 + l32;
     const int nsteps = nrounds * 9;
@@ -581,7 +591,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                 if constexpr (BF) {
                     bf16x8 fa[2], fb[2];
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) fa[i] = *(const bf16x8*)(halo + xswz(hb[i] + tofs, ch));
+                    for (int i = 0; i < 2; ++i) fa[i] = *(const bf16x8*)(halo + hswz(hb[i] + tofs, hrb[i] + ty, ch));
 #pragma unroll
                     for (int j = 0; j < 2; ++j) fb[j] = *(const bf16x8*)(wb + xswz(brow0 + 32 * j, ch));
 #pragma unroll
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     CFD_DASSERT(hb[i] + tofs < NPX);
-                    const int off = xswz(hb[i] + tofs, ch);
+                    const int off = hswz(hb[i] + tofs, hrb[i] + ty, ch);
                     fah[i] = *(const h8v*)(halo + off);
                     fal[i] = *(const h8v*)(halo + HPLANE + off);
                 }
