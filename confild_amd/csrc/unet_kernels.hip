@@ -1437,10 +1437,22 @@ __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, c
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, li = lane & 15;
-    const int h = blockIdx.y, heads = gridDim.y;
-    const int64_t b = blockIdx.z;
+    // linear workgroup L goes to XCD L % 8: with xcdmap the query tiles of one
+    // (sample, head) all get L % 8 == that group's XCD (the same queries, the same
+    // arithmetic: a schedule change only)
+    int qt = blockIdx.x, h = blockIdx.y;
+    int64_t b = blockIdx.z;
+    const int heads = gridDim.y;
+    if (a.xcdmap) {
+        const int nt = gridDim.x;
+        const int L = blockIdx.x + nt * (blockIdx.y + heads * blockIdx.z);
+        const int r = L >> 3, grp = (r / nt) * 8 + (L & 7);
+        qt = r - (r / nt) * nt;
+        h = grp % heads;
+        b = grp / heads;
+    }
     const int T = a.T, T32 = (T + 31) / 32 * 32;
-    const int q0 = (blockIdx.x * WAVES + wave) * 16;
+    const int q0 = (qt * WAVES + wave) * 16;
     const bool active = q0 < T;   // wave-uniform; an idle wave still stages and syncs
     CFD_DASSERT(h * CH + CH <= a.C);
     const int C3 = 3 * a.C;
@@ -2014,7 +2026,11 @@ void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* 
     // the parallelism of the 32^2 blocks (the choice changes no result: every
     // query's arithmetic is the same)
     static const int dma = env_int("CFD_ATTN_DMA", 1);
+    static const int xcdmap = env_int("CFD_ATTN_XCD", 1);   // (sample, head) workgroups on one XCD
     if (dma) {
+        AttnArgs a2 = a;
+        a2.xcdmap = xcdmap && (heads * B) % 8 == 0 ? 1 : 0;
+        const AttnArgs& a = a2;
         const int w8 = a.T >= 512 && (int64_t)B * heads * ceil_div(a.T, 128) >= 256;
         const dim3 grid((unsigned)ceil_div(a.T, w8 ? 128 : 64), heads, B);
         const dim3 blk(w8 ? 512 : 256);

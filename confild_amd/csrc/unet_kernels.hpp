@@ -75,6 +75,9 @@ struct AttnArgs {
     int T, C;
     float scale;       // 1/sqrt(sqrt(ch)), applied to q and k separately
     float* lse;        // optional (B, heads, T) log-sum-exp of each softmax row
+    // K4d: workgroups of one (sample, head) on one XCD (set by the launcher where
+    // heads * B % 8 == 0), so its K/V fragments are fetched into one L2
+    int xcdmap;
 };
 
 // GroupNorm(32)(+SiLU) backward: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),

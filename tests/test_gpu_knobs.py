@@ -6,7 +6,8 @@ in-workgroup K groups instead of two workgroups and a partial slab
 (CFD_CONV_KHG: 1 wherever it applies; default 0, never), the K1hb register
 build for two workgroups per CU (CFD_CONV_KHB_OCC, default on above 256
 workgroups: the 128^2 batch-5 case), the K1s / K1h epilogues through LDS
-(CFD_CONV_LDSEPI, default on) -- never the tiles' K order or the split-K boundaries, so every
+(CFD_CONV_LDSEPI, default on), the attention workgroups of one (sample, head)
+on one XCD (CFD_ATTN_XCD, default on) -- never the tiles' K order or the split-K boundaries, so every
 output's summation order, and hence eps, is unchanged.  Each setting runs in a
 child process (the switches are read once per process) over split-f16 U-Nets at
 the config-A and config-B widths, at batch 1 and 3 (the small-batch shapes these
@@ -59,7 +60,7 @@ def _run(env_extra):
 
 
 @pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0", "CFD_CONV_KHG=1",
-                                  "CFD_CONV_KHB_OCC=0", "CFD_CONV_LDSEPI=0"])
+                                  "CFD_CONV_KHB_OCC=0", "CFD_CONV_LDSEPI=0", "CFD_ATTN_XCD=0"])
 def test_schedule_switch_is_bit_identical(hip, knob):
     base = _run({})
     k, v = knob.split("=")
