@@ -724,6 +724,8 @@ struct ParamGrad {
     const float *temb = nullptr, *th1 = nullptr, *emb = nullptr;  // Tape's embedding activations
 };
 
+constexpr int kRangeSlots = 1024;   // zeroed once per parameter-gradient backward
+
 void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std::vector<Rec>& recs, Workspace& ws,
              hipStream_t st, const ParamGrad* pg = nullptr, bool pg_ws = false) {
     const auto& c = h->cfg;
@@ -756,7 +758,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         demb = ws.take((size_t)B * h->tdim);
         dth1 = ws.take((size_t)B * h->tdim);
         gpp = ws.take((size_t)B * cfd::kGnMaxChunks * 2 * cmax * 2);
-        wamax = (unsigned*)ws.take(64);   // the split weight gradient's operand ranges
+        wamax = (unsigned*)ws.take(kRangeSlots);   // the split weight gradients' operand ranges, a slot each
     }
     if (ws.dry) return;
     std::vector<size_t> goff;
@@ -772,9 +774,21 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         CFD_REQUIRE(it != h->index.end(), CFD_EKEY, "internal: no parameter " + key);
         return pg->grad + goff[it->second];
     };
-    // weight / bias gradient of one convolution: dY (B, Hout, Wout, cout) against its forward input
+    // split weight gradients: one zeroed range slot per operand range (max |dY|,
+    // max |X|); the GroupNorm backward's output carries its max |.| in a slot too
+    // (GnbArgs::amax_out), which a later weight gradient of that tensor reuses
+    int nslot = 0;
+    const bool split_w = pg && h->compute == CFD_COMPUTE_SPLIT_F16;
+    auto slot = [&]() -> unsigned* {
+        if (!split_w) return nullptr;
+        CFD_REQUIRE(nslot < kRangeSlots, CFD_ESTATE, "internal: range slots exhausted");
+        return wamax + nslot++;
+    };
+    // weight / bias gradient of one convolution: dY (B, Hout, Wout, cout) against its
+    // forward input; ymax: a slot already holding max |dY| (or null).  Returns the
+    // slot that holds max |dY| afterwards (for a later product of the same dY)
     auto wgrad = [&](const float* dy, int cout, const Act& X, const float* ss, int silu, int Hout, int Wout, int ks,
-                     int stride, int pad, int up, const std::string& pre) {
+                     int stride, int pad, int up, const std::string& pre, unsigned* ymax = nullptr) -> unsigned* {
         CFD_REQUIRE(pg_ws && cfd::colsum_part_floats((int64_t)B * Hout * Wout, cout, 1) <= ccap &&
                         (size_t)cout * X.C() * ks * ks <= wcap && (size_t)X.H * X.W * X.C() <= z.max_cat,
                     CFD_ESTATE, "internal: weight-gradient scratch");
@@ -792,7 +806,11 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         a.part = wpart;
         // split-f16 weight-gradient products in split compute (the exact fp32-MFMA
         // kernel in the fp32 / bf16 modes)
-        a.amax_out = h->compute == CFD_COMPUTE_SPLIT_F16 ? wamax : nullptr;
+        if (split_w) {
+            a.amax_x = slot();
+            a.ymax_known = ymax ? 1 : 0;
+            a.amax_y = ymax ? ymax : slot();
+        }
         a.P = (int64_t)B * Hout * Wout;
         a.Cout = cout;
         a.Hin = X.H;
@@ -806,8 +824,10 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         cfd::launch_conv_wgrad(a, GP(pre + ".weight"), st);
         cfd::launch_colsum(dy, a.P, cout, 1, cpart, crow, st);
         cfd::launch_rows_accum(crow, 1, cout, GP(pre + ".bias"), st);
+        return a.amax_y;
     };
     if (pg) CFD_HIP(hipMemsetAsync(demb, 0, sizeof(float) * B * h->tdim, st));
+    if (split_w) CFD_HIP(hipMemsetAsync(wamax, 0, sizeof(unsigned) * kRangeSlots, st));
 
     auto gfree = [&](const float* b1, const float* b2 = nullptr, const float* b3 = nullptr) -> float* {
         for (auto p : gpool)
@@ -850,7 +870,8 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     // with_param (training): the GroupNorm's parameter-gradient partials come out of
     // the same statistics pass (GnbArgs::ppart) and are accumulated into dgamma / dbeta
     auto gnb = [&](const Act& in, const float* ss, const float* stats, const std::string& pre, int silu,
-                   const float* dz, const float* addsrc, float* out1, float* out2, bool with_param = false) {
+                   const float* dz, const float* addsrc, float* out1, float* out2, bool with_param = false,
+                   unsigned* amax_out = nullptr) {
         cfd::GnbArgs g{};
         g.x1 = in.a;
         g.x2 = in.b;
@@ -869,12 +890,14 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         g.HW = in.H * in.W;
         g.silu = silu;
         if (with_param && pg) g.ppart = gpp;
+        g.amax_out = amax_out;
         const int nch = cfd::launch_gn_bwd(g, B, st);
         if (g.ppart)
             cfd::launch_gn_param_accum(gpp, B * nch, g.Ctot, GP(pre + ".weight"), GP(pre + ".bias"), st);
     };
 
     Act dcur;  // gradient w.r.t. the current activation (single contiguous tensor)
+    unsigned* dmax = nullptr;   // a range slot holding max |dcur| (split weight gradients), or null
     for (size_t si = h->steps.size(); si-- > 0;) {
         const auto& s = h->steps[si];
         const Rec& r = recs[si];
@@ -896,28 +919,33 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 a.tmode = 1;
                 cfd::launch_conv_in(a, st);
                 float* dh = gpool[1];
-                gnb(in, r.ss1, r.st1, "out.0", 1, G, nullptr, dh, nullptr, true);
+                unsigned* hm = slot();
+                gnb(in, r.ss1, r.st1, "out.0", 1, G, nullptr, dh, nullptr, true, hm);
                 if (pg) wgrad(d_eps, c.out_channels, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, "out.2");
                 dcur = Act{dh, in.Ca, nullptr, 0, in.H, in.W};
+                dmax = hm;
                 break;
             }
             case cfd::Step::Up: {
                 // nearest-2x + conv3x3 == one 4x4 stride-2 pad-1 convolution of dY (packed at set_param)
                 float* out = gfree(dcur.a);
-                if (pg) wgrad(dcur.a, dcur.Ca, in, nullptr, 0, dcur.H, dcur.W, 3, 1, 1, 1, s.conv);
+                if (pg) wgrad(dcur.a, dcur.Ca, in, nullptr, 0, dcur.H, dcur.W, 3, 1, 1, 1, s.conv, dmax);
                 dconv(dcur.a, dcur.Ca, dcur.H, dcur.W, s.conv + ".weight", s.cin, in.H, in.W, 4, 2, 1, 0, out);
                 dcur = Act{out, s.cin, nullptr, 0, in.H, in.W};
+                dmax = nullptr;
                 break;
             }
             case cfd::Step::Down: {
                 float* out = gfree(dcur.a);
-                if (pg) wgrad(dcur.a, dcur.Ca, in, nullptr, 0, dcur.H, dcur.W, 3, 2, 1, 0, s.conv);
+                if (pg) wgrad(dcur.a, dcur.Ca, in, nullptr, 0, dcur.H, dcur.W, 3, 2, 1, 0, s.conv, dmax);
                 dconv(dcur.a, dcur.Ca, dcur.H, dcur.W, s.conv + ".weight", s.cin, in.H, in.W, 3, 2, 1, 1, out);
                 dcur = Act{out, s.cin, nullptr, 0, in.H, in.W};
+                dmax = nullptr;
                 break;
             }
             case cfd::Step::Push:
                 // the pushed tensor's gradient also arrives through its skip concat
+                dmax = nullptr;   // dcur changes
                 cfd::launch_add(const_cast<float*>(dcur.a), dhs[r.push_hs], (int64_t)B * dcur.H * dcur.W * dcur.Ca,
                                 st);
                 break;
@@ -929,12 +957,14 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 float* G = gfree(dout);
                 // stride-1 3x3: plain convolutions with the mirrored packs (tpack 3)
                 const Act h1{r.h1, rs.cout, nullptr, 0, in.H, in.W};
-                if (pg) wgrad(dout, rs.cout, h1, r.ss2, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".out_layers.3");
+                unsigned* omax = dmax;   // max |dout| once known: shared by out_layers.3 and skip_connection
+                if (pg) omax = wgrad(dout, rs.cout, h1, r.ss2, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".out_layers.3", omax);
                 dconv(dout, rs.cout, in.H, in.W, rs.pre + ".out_layers.3.weight", rs.cout, in.H, in.W, 3, 1, 1, 0, G);
                 float* dh1 = gfree(dout, G);
-                gnb(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr, dh1, nullptr, true);
+                unsigned* h1max = slot();
+                gnb(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr, dh1, nullptr, true, h1max);
                 if (pg) {
-                    wgrad(dh1, rs.cout, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".in_layers.2");
+                    wgrad(dh1, rs.cout, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".in_layers.2", h1max);
                     // emb_layers: d emb_out[b, c] = sum over pixels of dh1; its Linear(SiLU(emb))
                     // backward, and the gradient w.r.t. emb accumulated over the ResBlocks
                     cfd::launch_colsum(dh1, (int64_t)in.H * in.W, rs.cout, B, cpart, crow, st);
@@ -948,16 +978,18 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 dconv(dh1, rs.cout, in.H, in.W, rs.pre + ".in_layers.2.weight", in.C(), in.H, in.W, 3, 1, 1, 0, G);
                 const float* addsrc = dout;
                 if (rs.cin != rs.cout) {
-                    if (pg) wgrad(dout, rs.cout, in, nullptr, 0, in.H, in.W, 1, 1, 0, 0, rs.pre + ".skip_connection");
+                    if (pg) wgrad(dout, rs.cout, in, nullptr, 0, in.H, in.W, 1, 1, 0, 0, rs.pre + ".skip_connection", omax);
                     float* sk = gfree(dout, G, dh1);
                     dconv(dout, rs.cout, in.H, in.W, rs.pre + ".skip_connection.weight", in.C(), in.H, in.W, 1, 1, 0,
                           0, sk);
                     addsrc = sk;
                 }
                 float* dx = dh1;  // dh1 is consumed: reuse for the first source's gradient
+                unsigned* xm = slot();
                 gnb(in, r.ss1, r.st1, rs.pre + ".in_layers.0", 1, G, addsrc, dx,
-                    in.b ? dhs[r.skip_hs] : nullptr, true);
+                    in.b ? dhs[r.skip_hs] : nullptr, true, xm);
                 dcur = Act{dx, in.Ca, nullptr, 0, in.H, in.W};
+                dmax = xm;
                 break;
             }
             case cfd::Step::Attn: {
@@ -967,7 +999,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 float* dA = gfree(dout);
                 if (pg)
                     wgrad(dout, at.C, Act{r.o, at.C, nullptr, 0, in.H, in.W}, nullptr, 0, in.H, in.W, 1, 1, 0, 0,
-                          at.pre + ".proj_out");
+                          at.pre + ".proj_out", dmax);
                 dconv(dout, at.C, in.H, in.W, at.pre + ".proj_out.weight", at.C, in.H, in.W, 1, 1, 0, 0, dA);
                 cfd::AttnBwdArgs ab{r.qkv, r.o, dA, r.lse, dd, dqkv, T, at.C,
                                     (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
@@ -975,14 +1007,16 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 if (pg) wgrad(dqkv, 3 * at.C, in, r.ss1, 0, in.H, in.W, 1, 1, 0, 0, at.pre + ".qkv");
                 float* dxn = gfree(dout, dA);
                 dconv(dqkv, 3 * at.C, in.H, in.W, at.pre + ".qkv.weight", at.C, in.H, in.W, 1, 1, 0, 0, dxn);
-                gnb(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn, dout, dA, nullptr, true);
+                unsigned* am = slot();
+                gnb(in, r.ss1, r.st1, at.pre + ".norm", 0, dxn, dout, dA, nullptr, true, am);
                 dcur = Act{dA, at.C, nullptr, 0, in.H, in.W};
+                dmax = am;
                 break;
             }
             case cfd::Step::In: {
                 if (pg) {
                     wgrad(dcur.a, dcur.Ca, Act{pg->x, c.in_channels, nullptr, 0, S, S}, nullptr, 0, S, S, 3, 1, 1, 0,
-                          s.conv);
+                          s.conv, dmax);
                     // time_embed: emb = L2(SiLU(L1(timestep_embedding(t)))) (unet.py:470-475,648)
                     cfd::launch_linear_wgrad(demb, pg->th1, B, h->tdim, h->tdim, 1, GP("time_embed.2.weight"),
                                              GP("time_embed.2.bias"), st);

@@ -99,6 +99,9 @@ struct GnbArgs {
     // optional (training): the GroupNorm parameter-gradient partials from the same
     // pass, (B, nchunks, Ctot, 2) floats = (sum dz_eff xhat, sum dz_eff) per chunk
     float* ppart;
+    // optional (training, split weight gradients): max |stored out1| reduced here
+    // with one atomicMax of the float bits per workgroup (a zeroed slot)
+    unsigned* amax_out;
     int C1, C2, Ctot, HW, silu, nchunks, B;
 };
 

@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
     const int ty = tap / a.ks, tx = tap - ty * a.ks;
     const int kbeg = (int)(blockIdx.z * a.kspan), kend = (int)min(a.P, (int64_t)kbeg + a.kspan);   // P < 2^31
     const int HWo = a.Hout * a.Wout, Wo = a.Wout, Ho = a.Hout;
-    const float sy = wg_scale(a.amax[0]), sx = wg_scale(a.amax[1]);
+    const float sy = wg_scale(*a.amax_y), sx = wg_scale(*a.amax_x);
     const int q = tid >> 3, ko = tid & 7;   // rows 4q..4q+3 (both operands), pixels 4ko..4ko+3 of a step
     const float rhw = 1.0f / (float)HWo, rw = 1.0f / (float)Wo;   // fdiv24: P < 2^24 (launch_conv_wgrad)
     // this block's X columns: one source, its row stride and channel offset
@@ -804,36 +804,33 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
         static const int split_env = getenv("CFD_WGRAD_SPLIT") ? atoi(getenv("CFD_WGRAD_SPLIT")) : 1;
         // fdiv24 pixel decode; 32-bit element offsets; one source per 128-column tile
         const int64_t srows0 = (int64_t)(a.P / ((int64_t)a.Hout * a.Wout)) * a.Hin * a.Win;
-        const bool split = split_env && a.amax_out && a.P < (1 << 24) && a.P * a.Cout < (1ll << 31) &&
+        const bool split = split_env && a.amax_y && a.amax_x && a.P < (1 << 24) && a.P * a.Cout < (1ll << 31) &&
                            srows0 * a.Ctot < (1ll << 31) && (a.ss || a.C2 == 0 || a.C1 % 128 == 0);
-        unsigned* amax = a.amax_out;
         auto absmax = [&](const float* x, int64_t n, unsigned* out) {
             const int64_t n4 = n / 4;
             hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(n4, 256)))),
                                dim3(256), 0, st, x, n4, out);
             check_launch("absmax_kernel");
         };
-        if (split) {
-            CFD_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned), st));
-            absmax(a.dy, a.P * a.Cout, amax);
-        }
+        // the range slots arrive zeroed (the caller zeroes its slot array once per
+        // backward and gives every range a slot of its own)
+        if (split && !a.ymax_known) absmax(a.dy, a.P * a.Cout, a.amax_y);
         const int64_t srows = (int64_t)(a.P / ((int64_t)a.Hout * a.Wout)) * a.Hin * a.Win;
         const float* act = nullptr;
         WgradArgs b = a;
         b.amax_out = nullptr;
-        b.amax = amax;
         if (a.ss) {
             CFD_REQUIRE(a.act, CFD_ESTATE, "internal: activation scratch");
             const int64_t nq = srows * (a.Ctot / 4);
             WgradArgs g = a;
-            g.amax_out = split ? amax + 1 : nullptr;
+            g.amax_out = split ? a.amax_x : nullptr;
             hipLaunchKernelGGL(gn_act_kernel, dim3((unsigned)std::min<int64_t>(4096, ceil_div(nq, 256))), dim3(256), 0, st,
                                g, nq);
             check_launch("gn_act_kernel");
             act = a.act;
         } else if (split) {
-            absmax(a.src1, srows * a.C1, amax + 1);
-            if (a.src2 && a.C2) absmax(a.src2, srows * a.C2, amax + 1);
+            absmax(a.src1, srows * a.C1, a.amax_x);
+            if (a.src2 && a.C2) absmax(a.src2, srows * a.C2, a.amax_x);
         }
         const dim3 grid((unsigned)(N / 128), (unsigned)ceil_div(a.Cout, 128), (unsigned)splits);
         if (split) {

@@ -17,10 +17,14 @@ struct WgradArgs {
     int C1, C2, Ctot, Cout;
     int Hin, Win, Hout, Wout;
     int ks, stride, pad, up, silu;
-    // split-f16 kernel: scratch for the two operand ranges (max |dY|, max |X| as
-    // float bits), written by the range pass and read by the product kernel
+    // split-f16 kernel: the two operand ranges (max |dY|, max |X| as float bits),
+    // each in a zeroed slot of its own (null: the exact fp32 kernel).  ymax_known:
+    // amax_y already holds max |dY| (written by the pass that produced dY), so no
+    // range pass over dY runs.  amax_out: where gn_act reduces max |X| (internal)
+    unsigned* amax_y;
+    unsigned* amax_x;
+    int ymax_known;
     unsigned* amax_out;
-    const unsigned* amax;
 };
 
 

@@ -176,15 +176,15 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(GnbArgs a) {
     const int64_t prow = i / cq;
     const int c0 = (int)(i - prow * cq) * 4;
     const int64_t nrow = (npix + GNB_PIX - 1) / GNB_PIX;
-    if (prow >= nrow) return;
     const int cpg = a.Ctot / 32;
     int64_t bcur = -1;
     GnbQuad k;
     f4 mg, mgx;
+    float mx = 0.f;   // max |stored out1| of this thread (a.amax_out)
 #pragma unroll
     for (int e = 0; e < GNB_PIX; ++e) {
         const int64_t pix = prow + e * nrow;
-        if (pix >= npix) break;
+        if (prow >= nrow || pix >= npix) break;
         const int64_t b = pix / a.HW;
         if (b != bcur) {
             bcur = b;
@@ -204,11 +204,21 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(GnbArgs a) {
         if (a.addsrc) dx += *(const f4*)(a.addsrc + pix * a.Ctot + c0);
         if (c0 < a.C1) {
             f4* o = (f4*)(a.out1 + pix * a.C1 + c0);
-            *o = a.acc1 ? *o + dx : dx;
+            const f4 v = a.acc1 ? *o + dx : dx;
+            *o = v;
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         } else {
             f4* o = (f4*)(a.out2 + pix * a.C2 + (c0 - a.C1));
             *o = a.acc2 ? *o + dx : dx;
         }
+    }
+    if (a.amax_out) {   // block-uniform
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        __shared__ float wm[4];
+        if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(a.amax_out, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
     }
 }
 
