@@ -745,7 +745,8 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     float *wpart = nullptr, *cpart = nullptr, *crow = nullptr, *demb = nullptr, *dth1 = nullptr, *gpp = nullptr;
     float* wact = nullptr;
     unsigned* wamax = nullptr;
-    size_t wcap = 0, ccap = 0;
+    float* wbpart = nullptr;
+    size_t wcap = 0, ccap = 0, bcap = 0;
     if (pg_ws) {
         int cmax = 0;
         for (int l = 0; l < c.n_mult; ++l) cmax = std::max(cmax, c.channel_mult[l] * c.model_channels);
@@ -759,6 +760,8 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         dth1 = ws.take((size_t)B * h->tdim);
         gpp = ws.take((size_t)B * cfd::kGnMaxChunks * 2 * cmax * 2);
         wamax = (unsigned*)ws.take(kRangeSlots);   // the split weight gradients' operand ranges, a slot each
+        bcap = (size_t)64 * 3 * cmax;
+        wbpart = ws.take(bcap);   // bias-gradient slices of the split product kernel
     }
     if (ws.dry) return;
     std::vector<size_t> goff;
@@ -821,9 +824,13 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         a.stride = stride;
         a.pad = pad;
         a.up = up;
-        cfd::launch_conv_wgrad(a, GP(pre + ".weight"), st);
-        cfd::launch_colsum(dy, a.P, cout, 1, cpart, crow, st);
-        cfd::launch_rows_accum(crow, 1, cout, GP(pre + ".bias"), st);
+        a.bpart = wbpart;
+        a.bpart_cap = (int64_t)bcap;
+        a.Gb = GP(pre + ".bias");
+        if (!cfd::launch_conv_wgrad(a, GP(pre + ".weight"), st)) {   // the bias gradient not fused: sum dY
+            cfd::launch_colsum(dy, a.P, cout, 1, cpart, crow, st);
+            cfd::launch_rows_accum(crow, 1, cout, GP(pre + ".bias"), st);
+        }
         return a.amax_y;
     };
     if (pg) CFD_HIP(hipMemsetAsync(demb, 0, sizeof(float) * B * h->tdim, st));

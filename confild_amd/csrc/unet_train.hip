@@ -318,6 +318,10 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
     const int iyo = UP ? ty - a.pad : ty - a.pad, ixo = UP ? tx - a.pad : tx - a.pad;
     const int Hlim = UP ? 2 * a.Hin : a.Hin, Wlim = UP ? 2 * a.Win : a.Win;
     f4 yv[4], xv[4];   // [pixel]: 4 rows each
+    // bias gradient (a.bpart, the tap-0 column blocks): this thread's rows summed
+    // over its pixels in load order, fp32
+    const bool bias = a.bpart && blockIdx.x == 0;
+    f4 bsum = f4{0.f, 0.f, 0.f, 0.f};
     auto load = [&](int k0) {
         const int kb = k0 + 4 * ko;          // the thread's first pixel; the next 3 follow it
         int b = fdiv24(kb, HWo, rhw);
@@ -345,6 +349,7 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
             yv[p] = y;
             xv[p] = x;
         }
+        if (bias) bsum = ((bsum + yv[0]) + yv[1]) + (yv[2] + yv[3]);
     };
     // transpose in registers: row r = 4q + i gets pixels 4ko..4ko+3 of both operands
     auto store = [&](int buf) {
@@ -402,6 +407,19 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
             __syncthreads();
             cur ^= 1;
         }
+    }
+    if (bias) {   // the 8 pixel lanes of a row quad (consecutive lanes) in lane order
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            f4 t;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = __shfl_xor(bsum[e], o);
+            bsum = (ko & o) ? t + bsum : bsum + t;
+        }
+        if (ko == 0)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (m0 + 4 * q + e < M) a.bpart[(int64_t)blockIdx.z * M + m0 + 4 * q + e] = bsum[e];
     }
     const float unscale = 1.f / (sx * sy);   // exact: a power of two
     float* Cz = a.part + (int64_t)blockIdx.z * M * N;
@@ -537,9 +555,15 @@ __global__ __launch_bounds__(1024) void conv_wgrad_thin_kernel(WgradArgs a) {
 
 // G[co][ci][tap] (the reference weight layout) += sum_z part[z][co][tap * Ctot + ci]
 __global__ __launch_bounds__(256) void wgrad_accum_kernel(const float* __restrict__ part, int Cout, int Ctot, int taps,
-                                                          int splits, float* __restrict__ G) {
+                                                          int splits, float* __restrict__ G,
+                                                          const float* __restrict__ bpart, float* __restrict__ Gb) {
     const int64_t MN = (int64_t)Cout * Ctot * taps;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // index in G
+    if (bpart && i < Cout) {   // the bias gradient's slices in slice order
+        float sb = bpart[i];
+        for (int z = 1; z < splits; ++z) sb += bpart[(int64_t)z * Cout + i];
+        Gb[i] = Gb[i] + sb;
+    }
     if (i >= MN) return;
     const int64_t co = i / ((int64_t)Ctot * taps);
     const int rem = (int)(i - co * Ctot * taps), ci = rem / taps, tap = rem - ci * taps;
@@ -793,9 +817,10 @@ size_t wgrad_part_floats(const WgradArgs& a) {
     return (size_t)((a.P + span - 1) / span) * a.Cout * a.Ctot * a.ks * a.ks;
 }
 
-void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
+bool launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
     a.kspan = wgrad_kspan(a);
     const int splits = (int)((a.P + a.kspan - 1) / a.kspan);
+    bool bias_fused = false;
     const int N = a.ks * a.ks * a.Ctot;
     CFD_REQUIRE(wgrad_part_floats(a) <= (size_t)a.part_cap, CFD_ESTATE, "internal: weight-gradient scratch");
     if (wgrad_fast(a)) {
@@ -833,6 +858,8 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
             if (a.src2 && a.C2) absmax(a.src2, srows * a.C2, a.amax_x);
         }
         const dim3 grid((unsigned)(N / 128), (unsigned)ceil_div(a.Cout, 128), (unsigned)splits);
+        if (!split || !a.Gb || (int64_t)splits * a.Cout > a.bpart_cap) b.bpart = nullptr;
+        bias_fused = b.bpart != nullptr;
         if (split) {
             if (a.up)
                 hipLaunchKernelGGL(conv_wgrad128_split_kernel<true>, grid, dim3(256), 0, st, b, act);
@@ -861,9 +888,10 @@ void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
         check_launch("conv_wgrad_kernel");
     }
     const int64_t MN = (int64_t)a.Cout * N;
-    hipLaunchKernelGGL(wgrad_accum_kernel, dim3((unsigned)ceil_div(MN, 256)), dim3(256), 0, st, a.part, a.Cout,
-                       a.Ctot, a.ks * a.ks, splits, G);
+    hipLaunchKernelGGL(wgrad_accum_kernel, dim3((unsigned)ceil_div(std::max<int64_t>(MN, a.Cout), 256)), dim3(256), 0, st,
+                       a.part, a.Cout, a.Ctot, a.ks * a.ks, splits, G, bias_fused ? a.bpart : nullptr, a.Gb);
     check_launch("wgrad_accum_kernel");
+    return bias_fused;
 }
 
 namespace {

@@ -25,14 +25,21 @@ struct WgradArgs {
     unsigned* amax_x;
     int ymax_known;
     unsigned* amax_out;
+    // optional: the bias gradient (sum of dY over the pixels) from the split
+    // product kernel's dY loads -- bpart scratch (slices x Cout floats), Gb += it.
+    // launch_conv_wgrad returns whether it took it (else the caller sums dY)
+    float* bpart;
+    int64_t bpart_cap;
+    float* Gb;
 };
 
 
 // pixel slice of one block (P, Cout, Ctot, ks and part_cap of a set)
 int64_t wgrad_kspan(const WgradArgs& a);
 size_t wgrad_part_floats(const WgradArgs& a);
-// G (Cout, Ctot, ks, ks) += dW
-void launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st);
+// G (Cout, Ctot, ks, ks) += dW; returns true when it also added the bias gradient
+// into a.Gb (the split kernel with a.bpart / a.Gb set)
+bool launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st);
 size_t colsum_part_floats(int64_t n, int64_t F, int R);
 // out (R, F) = per-row-group column sums of X (R groups of n rows of F)
 void launch_colsum(const float* X, int64_t n, int64_t F, int R, float* part, float* out, hipStream_t st);
