@@ -315,6 +315,10 @@ struct Rec {
     float *ss1 = nullptr, *st1 = nullptr;  // first GroupNorm: scale/shift, mean/rstd
     float *ss2 = nullptr, *st2 = nullptr;  // Res: out_layers GroupNorm
     float *qkv = nullptr, *o = nullptr, *lse = nullptr;  // Attn
+    // with a tape: the GroupNorm(+SiLU) outputs the next convolutions read, kept,
+    // and a slot with max |.| of each (the split weight gradients' X ranges)
+    const float *act1 = nullptr, *act2 = nullptr;
+    unsigned *amx1 = nullptr, *amx2 = nullptr;
     int skip_hs = -1;               // Res on a concat: skip-stack index of the second source
     int push_hs = -1;               // Push: skip-stack index
 };
@@ -410,8 +414,12 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     // skip stack buffers (one per Push); in the tape when recording
     std::vector<float*> hsbuf;
     for (size_t n : z.hs) hsbuf.push_back(tape ? tape->tws->take((size_t)B * n) : ws.take((size_t)B * n));
+    constexpr int kGnSlots = 256;   // the kept GroupNorm outputs' range slots (tape)
+    unsigned* gslots = tape ? (unsigned*)tape->tws->take(kGnSlots) : nullptr;
+    int ngs = 0;
     if (ws.dry && !tape) return;
     auto keep = [&](size_t nfloats) -> float* { return tape->tws->take(nfloats); };
+    if (tape && launch) CFD_HIP(hipMemsetAsync(gslots, 0, sizeof(unsigned) * kGnSlots, st));
     std::vector<Rec>* recs = tape ? tape->recs : nullptr;
     if (recs) recs->assign(h->steps.size(), Rec{});
 
@@ -450,7 +458,8 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     // nothing else, so it is not stored (the GroupNorm of in_layers' output
     // without a tape)
     auto gn = [&](const Act& in, const std::string& pre, int silu, float** ss, float** stats,
-                  bool keep_raw = true, bool bf16_out = false) -> Act {
+                  bool keep_raw = true, bool bf16_out = false, const float** actp = nullptr,
+                  unsigned** amxp = nullptr) -> Act {
         cfd::GnArgs g{};
         g.src1 = in.a;
         g.src2 = in.b;
@@ -463,6 +472,13 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             *stats = g.stats = keep((size_t)B * 64);
         }
         g.out = nbuf;
+        if (tape && actp) {   // kept for the weight gradients, with its range
+            CFD_REQUIRE(!bf16_out && ngs < kGnSlots, CFD_ESTATE, "internal: kept GroupNorm output");
+            g.out = keep((size_t)B * in.H * in.W * in.C());
+            g.amax_out = gslots + ngs++;
+            *actp = g.out;
+            *amxp = g.amax_out;
+        }
         g.C1 = in.Ca;
         g.C2 = in.Cb;
         g.Ctot = in.C();
@@ -487,7 +503,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     g.C2, g.kpart ? g.ksplits : 0, g.kres ? 1 : 0, g.kx ? 1 : 0, silu);
         g.out_bf16 = bf16_out ? 1 : 0;
         if (launch) cfd::launch_gn(g, B, st);
-        Act r{nbuf, in.C(), nullptr, 0, in.H, in.W};
+        Act r{g.out, in.C(), nullptr, 0, in.H, in.W};
         r.bf16 = bf16_out;
         return r;
     };
@@ -617,7 +633,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 const size_t nout = (size_t)B * cur.H * cur.W * r.cout;
                 // h = in_layers(x) + emb_layers(emb)   (unet.py:236-254)
                 const Act xin = gn(cur, r.pre + ".in_layers.0", 1, &rec.ss1, &rec.st1, true,
-                                   feeds_k1hb(cur, r.pre + ".in_layers.2", r.cout));
+                                   feeds_k1hb(cur, r.pre + ".in_layers.2", r.cout), &rec.act1, &rec.amx1);
                 // skip(x) first (its split-K reduction is flushed by the next
                 // convolution), so that in_layers' deferred reduction meets the
                 // out_layers GroupNorm directly   (unet.py:255-256)
@@ -634,7 +650,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 rec.h1 = hb;
                 const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
                 const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2, /*keep_raw=*/tape != nullptr,
-                                  feeds_k1hb(th, r.pre + ".out_layers.3", r.cout));
+                                  feeds_k1hb(th, r.pre + ".out_layers.3", r.cout), &rec.act2, &rec.amx2);
                 float* out = dest(cur.a, cur.b, nout);
                 conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};
@@ -643,7 +659,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             case cfd::Step::Attn: {
                 const auto& at = h->attn[s.idx];
                 const int T = cur.H * cur.W;
-                const Act xn = gn(cur, at.pre + ".norm", 0, &rec.ss1, &rec.st1);
+                const Act xn = gn(cur, at.pre + ".norm", 0, &rec.ss1, &rec.st1, true, false, &rec.act1, &rec.amx1);
                 float* qb = tape ? keep((size_t)B * T * 3 * at.C) : qkv;
                 float* ob = tape ? keep((size_t)B * T * at.C) : abuf;
                 conv(xn, at.pre + ".qkv", 3 * at.C, 1, 1, 0, nullptr, nullptr, qb);
@@ -683,7 +699,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 break;
             }
             case cfd::Step::Out: {
-                const Act on = gn(cur, "out.0", 1, &rec.ss1, &rec.st1);
+                const Act on = gn(cur, "out.0", 1, &rec.ss1, &rec.st1, true, false, &rec.act1, &rec.amx1);
                 cfd::ConvArgs a{};
                 a.src1 = on.a;
                 a.C1 = on.Ca;
@@ -791,7 +807,8 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     // forward input; ymax: a slot already holding max |dY| (or null).  Returns the
     // slot that holds max |dY| afterwards (for a later product of the same dY)
     auto wgrad = [&](const float* dy, int cout, const Act& X, const float* ss, int silu, int Hout, int Wout, int ks,
-                     int stride, int pad, int up, const std::string& pre, unsigned* ymax = nullptr) -> unsigned* {
+                     int stride, int pad, int up, const std::string& pre, unsigned* ymax = nullptr,
+                     unsigned* xmax = nullptr) -> unsigned* {
         CFD_REQUIRE(pg_ws && cfd::colsum_part_floats((int64_t)B * Hout * Wout, cout, 1) <= ccap &&
                         (size_t)cout * X.C() * ks * ks <= wcap && (size_t)X.H * X.W * X.C() <= z.max_cat,
                     CFD_ESTATE, "internal: weight-gradient scratch");
@@ -810,7 +827,8 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         // split-f16 weight-gradient products in split compute (the exact fp32-MFMA
         // kernel in the fp32 / bf16 modes)
         if (split_w) {
-            a.amax_x = slot();
+            a.xmax_known = xmax ? 1 : 0;
+            a.amax_x = xmax ? xmax : slot();
             a.ymax_known = ymax ? 1 : 0;
             a.amax_y = ymax ? ymax : slot();
         }
@@ -928,7 +946,13 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 float* dh = gpool[1];
                 unsigned* hm = slot();
                 gnb(in, r.ss1, r.st1, "out.0", 1, G, nullptr, dh, nullptr, true, hm);
-                if (pg) wgrad(d_eps, c.out_channels, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, "out.2");
+                if (pg) {
+                    if (r.act1)   // the kept GroupNorm(+SiLU) output and its range
+                        wgrad(d_eps, c.out_channels, Act{r.act1, in.C(), nullptr, 0, in.H, in.W}, nullptr, 0, in.H,
+                              in.W, 3, 1, 1, 0, "out.2", nullptr, r.amx1);
+                    else
+                        wgrad(d_eps, c.out_channels, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, "out.2");
+                }
                 dcur = Act{dh, in.Ca, nullptr, 0, in.H, in.W};
                 dmax = hm;
                 break;
@@ -965,13 +989,21 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 // stride-1 3x3: plain convolutions with the mirrored packs (tpack 3)
                 const Act h1{r.h1, rs.cout, nullptr, 0, in.H, in.W};
                 unsigned* omax = dmax;   // max |dout| once known: shared by out_layers.3 and skip_connection
-                if (pg) omax = wgrad(dout, rs.cout, h1, r.ss2, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".out_layers.3", omax);
+                if (pg)
+                    omax = r.act2 ? wgrad(dout, rs.cout, Act{r.act2, rs.cout, nullptr, 0, in.H, in.W}, nullptr, 0, in.H,
+                                          in.W, 3, 1, 1, 0, rs.pre + ".out_layers.3", omax, r.amx2)
+                                  : wgrad(dout, rs.cout, h1, r.ss2, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".out_layers.3",
+                                          omax);
                 dconv(dout, rs.cout, in.H, in.W, rs.pre + ".out_layers.3.weight", rs.cout, in.H, in.W, 3, 1, 1, 0, G);
                 float* dh1 = gfree(dout, G);
                 unsigned* h1max = slot();
                 gnb(h1, r.ss2, r.st2, rs.pre + ".out_layers.0", 1, G, nullptr, dh1, nullptr, true, h1max);
                 if (pg) {
-                    wgrad(dh1, rs.cout, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".in_layers.2", h1max);
+                    if (r.act1)
+                        wgrad(dh1, rs.cout, Act{r.act1, in.C(), nullptr, 0, in.H, in.W}, nullptr, 0, in.H, in.W, 3, 1, 1,
+                              0, rs.pre + ".in_layers.2", h1max, r.amx1);
+                    else
+                        wgrad(dh1, rs.cout, in, r.ss1, 1, in.H, in.W, 3, 1, 1, 0, rs.pre + ".in_layers.2", h1max);
                     // emb_layers: d emb_out[b, c] = sum over pixels of dh1; its Linear(SiLU(emb))
                     // backward, and the gradient w.r.t. emb accumulated over the ResBlocks
                     cfd::launch_colsum(dh1, (int64_t)in.H * in.W, rs.cout, B, cpart, crow, st);
@@ -1011,7 +1043,13 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 cfd::AttnBwdArgs ab{r.qkv, r.o, dA, r.lse, dd, dqkv, T, at.C,
                                     (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
                 cfd::launch_attention_bwd(ab, at.ch, at.heads, B, st);
-                if (pg) wgrad(dqkv, 3 * at.C, in, r.ss1, 0, in.H, in.W, 1, 1, 0, 0, at.pre + ".qkv");
+                if (pg) {
+                    if (r.act1)
+                        wgrad(dqkv, 3 * at.C, Act{r.act1, at.C, nullptr, 0, in.H, in.W}, nullptr, 0, in.H, in.W, 1, 1, 0,
+                              0, at.pre + ".qkv", nullptr, r.amx1);
+                    else
+                        wgrad(dqkv, 3 * at.C, in, r.ss1, 0, in.H, in.W, 1, 1, 0, 0, at.pre + ".qkv");
+                }
                 float* dxn = gfree(dout, dA);
                 dconv(dqkv, 3 * at.C, in.H, in.W, at.pre + ".qkv.weight", at.C, in.H, in.W, 1, 1, 0, 0, dxn);
                 unsigned* am = slot();

@@ -147,27 +147,50 @@ __device__ __forceinline__ void gn_store4(const GnArgs& a, int64_t e, const f4& 
         *(f4*)(a.out + e) = y;
 }
 
+// every thread of the workgroup calls it: max of mx over the workgroup, then one
+// atomicMax of its float bits (non-negative: the integer order is the float order)
+__device__ __forceinline__ void block_amax_atomic(float mx, unsigned* out) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    __shared__ float wmx[16];
+    const int nw = (blockDim.x + 63) >> 6;
+    if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = wmx[0];
+        for (int w = 1; w < nw; ++w) m = fmaxf(m, wmx[w]);
+        atomicMax(out, __float_as_uint(m));
+    }
+}
+__device__ __forceinline__ float amax4(const f4& y) {
+    return fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3])));
+}
+
 // y = x*scale + shift (+ SiLU), one float4 per thread, written as one
 // contiguous (B, HW, Ctot) tensor (the concat of two sources materialised here).
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
     const int cq = a.Ctot / 4;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)a.B * a.HW * cq) return;
-    const int64_t pix = i / cq;
-    const int c0 = (int)(i - pix * cq) * 4;
-    const int64_t b = pix / a.HW;
-    f4 v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0) : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
-    const float* ss = a.ss + (b * a.Ctot + c0) * 2;
-    const f4 s01 = *(const f4*)ss, s23 = *(const f4*)(ss + 4);
-    v[0] = v[0] * s01[0] + s01[1];
-    v[1] = v[1] * s01[2] + s01[3];
-    v[2] = v[2] * s23[0] + s23[1];
-    v[3] = v[3] * s23[2] + s23[3];
-    if (a.silu) {
+    float mx = 0.f;
+    if (i < (int64_t)a.B * a.HW * cq) {
+        const int64_t pix = i / cq;
+        const int c0 = (int)(i - pix * cq) * 4;
+        const int64_t b = pix / a.HW;
+        f4 v = c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0) : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
+        const float* ss = a.ss + (b * a.Ctot + c0) * 2;
+        const f4 s01 = *(const f4*)ss, s23 = *(const f4*)(ss + 4);
+        v[0] = v[0] * s01[0] + s01[1];
+        v[1] = v[1] * s01[2] + s01[3];
+        v[2] = v[2] * s23[0] + s23[1];
+        v[3] = v[3] * s23[2] + s23[3];
+        if (a.silu) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
+            for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
+        }
+        gn_store4(a, pix * a.Ctot + c0, v);
+        mx = amax4(v);
     }
-    gn_store4(a, pix * a.Ctot + c0, v);
+    if (a.amax_out) block_amax_atomic(mx, a.amax_out);
 }
 
 // K3f: the same GroupNorm(+SiLU) in ONE launch: workgroup = (sample, group).
@@ -234,23 +257,27 @@ __global__ __launch_bounds__(256) void gn_fused_kernel(GnArgs a) {
         }
     }
     __syncthreads();
-    if (!act) return;
-    f4 sc, sf;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        sc[j] = sh[0][4 * q + j];
-        sf[j] = sh[1][4 * q + j];
-    }
-    const int64_t dst = b * HW * Ctot + c;
-    for (int p = r0; p < HW; p += rows) {
-        f4 v = *(const f4*)(src + (int64_t)p * ld);
+    float mx = 0.f;
+    if (act) {
+        f4 sc, sf;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            v[j] = v[j] * sc[j] + sf[j];
-            if (a.silu) v[j] = silu_f(v[j]);
+            sc[j] = sh[0][4 * q + j];
+            sf[j] = sh[1][4 * q + j];
         }
-        gn_store4(a, dst + (int64_t)p * Ctot, v);
+        const int64_t dst = b * HW * Ctot + c;
+        for (int p = r0; p < HW; p += rows) {
+            f4 v = *(const f4*)(src + (int64_t)p * ld);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = v[j] * sc[j] + sf[j];
+                if (a.silu) v[j] = silu_f(v[j]);
+            }
+            gn_store4(a, dst + (int64_t)p * Ctot, v);
+            mx = fmaxf(mx, amax4(v));
+        }
     }
+    if (a.amax_out) block_amax_atomic(mx, a.amax_out);
 }
 
 // Register-resident form for HW x cpg <= 512 x IPT x 4: 512 threads, each
@@ -403,27 +430,31 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     }
     __syncthreads();
     CFD_STAMP(a.stamps, 4, a.seq, 2);
-    if (!act) return;
-    f4 sc, sf;
+    float mx = 0.f;
+    if (act) {
+        f4 sc, sf;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        sc[j] = sh[0][4 * q + j];
-        sf[j] = sh[1][4 * q + j];
-    }
-    const int64_t dst = b * HW * Ctot + c;
+        for (int j = 0; j < 4; ++j) {
+            sc[j] = sh[0][4 * q + j];
+            sf[j] = sh[1][4 * q + j];
+        }
+        const int64_t dst = b * HW * Ctot + c;
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        const int p = r0 + k * rows;
-        if (p < HW) {
-            f4 y;
+        for (int k = 0; k < IPT; ++k) {
+            const int p = r0 + k * rows;
+            if (p < HW) {
+                f4 y;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                y[j] = v[k][j] * sc[j] + sf[j];
-                if (a.silu) y[j] = silu_f(y[j]);
+                for (int j = 0; j < 4; ++j) {
+                    y[j] = v[k][j] * sc[j] + sf[j];
+                    if (a.silu) y[j] = silu_f(y[j]);
+                }
+                gn_store4(a, dst + (int64_t)p * Ctot, y);
+                mx = fmaxf(mx, amax4(y));
             }
-            gn_store4(a, dst + (int64_t)p * Ctot, y);
         }
     }
+    if (a.amax_out) block_amax_atomic(mx, a.amax_out);
 #ifdef CFD_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
 #endif

@@ -35,6 +35,10 @@ struct GnArgs {
     // config E, where the consumer is a K1hb convolution that rounds its operand
     // to bf16 anyway -- the same bits, half the bytes written and re-read
     int out_bf16;
+    // optional (training tape): max |stored out| reduced into this zeroed slot, one
+    // atomicMax of the float bits per workgroup -- the operand range the split
+    // weight gradients of the next convolution need
+    unsigned* amax_out;
 };
 
 struct ConvArgs {

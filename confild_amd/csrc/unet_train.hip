@@ -853,7 +853,7 @@ bool launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
                                g, nq);
             check_launch("gn_act_kernel");
             act = a.act;
-        } else if (split) {
+        } else if (split && !a.xmax_known) {
             absmax(a.src1, srows * a.C1, a.amax_x);
             if (a.src2 && a.C2) absmax(a.src2, srows * a.C2, a.amax_x);
         }

@@ -24,6 +24,7 @@ struct WgradArgs {
     unsigned* amax_y;
     unsigned* amax_x;
     int ymax_known;
+    int xmax_known;   // amax_x already holds max |X| (the forward GroupNorm kept X and its range)
     unsigned* amax_out;
     // optional: the bias gradient (sum of dY over the pixels) from the split
     // product kernel's dY loads -- bpart scratch (slices x Cout floats), Gb += it.
