@@ -472,7 +472,9 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             *stats = g.stats = keep((size_t)B * 64);
         }
         g.out = nbuf;
-        if (tape && actp) {   // kept for the weight gradients, with its range
+        // CFD_TAPE_GNOUT=0: the weight gradients recompute the activated input instead
+        static const int tape_gnout = getenv("CFD_TAPE_GNOUT") ? atoi(getenv("CFD_TAPE_GNOUT")) : 1;
+        if (tape && actp && tape_gnout) {   // kept for the weight gradients, with its range
             CFD_REQUIRE(!bf16_out && ngs < kGnSlots, CFD_ESTATE, "internal: kept GroupNorm output");
             g.out = keep((size_t)B * in.H * in.W * in.C());
             g.amax_out = gslots + ngs++;
