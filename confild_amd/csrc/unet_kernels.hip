@@ -170,9 +170,10 @@ __device__ __forceinline__ float amax4(const f4& y) {
 // contiguous (B, HW, Ctot) tensor (the concat of two sources materialised here).
 __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
     const int cq = a.Ctot / 4;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float mx = 0.f;
-    if (i < (int64_t)a.B * a.HW * cq) {
+    // grid-stride over float4 quads (a bounded grid: one range atomic per workgroup)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)a.B * a.HW * cq;
+         i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t pix = i / cq;
         const int c0 = (int)(i - pix * cq) * 4;
         const int64_t b = pix / a.HW;
@@ -1749,7 +1750,7 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(1024), 0, st, a);
     check_launch("gn_finalize_kernel");
     const int64_t nq = (int64_t)B * a.HW * a.Ctot / 4;
-    hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)std::min<int64_t>(4096, ceil_div(nq, 256))), dim3(256), 0, st, a);
     check_launch("gn_apply_kernel");
 }
 
