@@ -283,11 +283,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int d = 0; d < ND; ++d) dQ[d] = f4{0.f, 0.f, 0.f, 0.f};
     for (int kb = 0; kb < T; kb += 16) {
-        // S^T and dP^T each as two interleaved accumulation chains (even / odd
-        // channel quads), added at the end: four independent MFMA chains in flight
-        // instead of two dependent ones
         f4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
-        f4 st1 = {0.f, 0.f, 0.f, 0.f}, dpt1 = {0.f, 0.f, 0.f, 0.f};
         {
             const float* kp = base + (int64_t)(kb + li) * C3 + CH + KQ * g;
             const float* vp = kp + CH;
@@ -296,16 +292,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
                 const f4 kv = *(const f4*)(kp + s);
                 const f4 vv = *(const f4*)(vp + s);
 #pragma unroll
-                for (int u = 0; u < 4; u += 2) {
+                for (int u = 0; u < 4; ++u) {
                     st = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[u] * scale, qf[s + u], st, 0, 0, 0);
                     dpt = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[u], df[s + u], dpt, 0, 0, 0);
-                    st1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[u + 1] * scale, qf[s + u + 1], st1, 0, 0, 0);
-                    dpt1 = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[u + 1], df[s + u + 1], dpt1, 0, 0, 0);
                 }
             }
         }
-        st += st1;
-        dpt += dpt1;
         // lane (g, li): S[query li][key kb + 4g + r], dP likewise
         float ds[4];
 #pragma unroll
@@ -359,9 +351,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int d = 0; d < ND; ++d) dK[d] = dV[d] = f4{0.f, 0.f, 0.f, 0.f};
     for (int qb = 0; qb < T; qb += 16) {
-        // two interleaved chains each for S and dP (see attn_bwd_dq_kernel)
         f4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-        f4 st1 = {0.f, 0.f, 0.f, 0.f}, dp1 = {0.f, 0.f, 0.f, 0.f};
         {
             const float* qp = base + (int64_t)(qb + li) * C3 + KQ * g;
             const float* dop = dbase + (int64_t)(qb + li) * a.C + KQ * g;
@@ -370,16 +360,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
                 const f4 qv = *(const f4*)(qp + s);
                 const f4 dv = *(const f4*)(dop + s);
 #pragma unroll
-                for (int u = 0; u < 4; u += 2) {
+                for (int u = 0; u < 4; ++u) {
                     st = __builtin_amdgcn_mfma_f32_16x16x4f32(qv[u] * scale, kf[s + u], st, 0, 0, 0);
                     dp = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[u], vf[s + u], dp, 0, 0, 0);
-                    st1 = __builtin_amdgcn_mfma_f32_16x16x4f32(qv[u + 1] * scale, kf[s + u + 1], st1, 0, 0, 0);
-                    dp1 = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[u + 1], vf[s + u + 1], dp1, 0, 0, 0);
                 }
             }
         }
-        st += st1;
-        dp += dp1;
         // lane (g, li): S[query qb + 4g + r][key li]
         float p[4], ds[4];
         {
