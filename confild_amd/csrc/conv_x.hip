@@ -894,14 +894,7 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         return splits;
     }
     switch (variant) {
-        case 1: {   // CFD_CONVX_PF=2 (development): two K tiles in flight (same tiles, same sums)
-            static const int pf = getenv("CFD_CONVX_PF") ? atoi(getenv("CFD_CONVX_PF")) : 1;
-            if (pf == 2)
-                hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1, 2>), grid(128, 128), dim3(256), 0, st, a);
-            else
-                hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1>), grid(128, 128), dim3(256), 0, st, a);
-            break;
-        }
+        case 1: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1>), grid(128, 128), dim3(256), 0, st, a); break;
         case 2: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1>), grid(256, 128), dim3(512), 0, st, a); break;
         default: CFD_REQUIRE(false, CFD_EARG, "conv_x variant");
     }
