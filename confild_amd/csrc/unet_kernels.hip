@@ -1719,14 +1719,12 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     CFD_REQUIRE(!a.kpart || gn_takes_splitk(a, B), CFD_ESTATE, "internal: split-K source on a GroupNorm path without it");
     static const int fused = env_int("CFD_GN_FUSED", 1);
     static const int big = env_int("CFD_GN_BIG", 1);   // 0: the one-launch kernels at every size
-    // register slots per thread above which the three-kernel path takes over
-    static const int big_ipt = env_int("CFD_GN_BIG_IPT", 32);
     static const int nt1024 = env_int("CFD_GN_NT1024", 1);
     const int ipt = a.Ctot % 128 == 0 ? (int)ceil_div(a.HW, 512 / (a.Ctot / 128)) : 0;
     // large latents (ipt > 32): a workgroup per (sample, group) would leave the
     // chip idle at small batch (32 workgroups at B = 1, 384^2), so they take the
     // three-kernel path below, whose statistics spread over gn_chunks(HW) chunks
-    if (fused && a.Ctot % 128 == 0 && !(big && ipt > big_ipt && fused != 2)) {
+    if (fused && a.Ctot % 128 == 0 && !(big && ipt > 32 && fused != 2)) {
         const dim3 grid((unsigned)(32 * B));
         if (fused == 2 || ipt > 32)
             hipLaunchKernelGGL(gn_fused_kernel, grid, dim3(256), 0, st, a);
