@@ -62,6 +62,7 @@ _SIGS = {
                                         C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]),
     "cfd_unet_input_vjp": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t,
                                      C.c_void_p, C.c_size_t, C.c_void_p]),
+    "cfd_unet_set_tape_mode": (C.c_int, [C.c_void_p, C.c_int]),
     "cfd_sched_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "cfd_sched_destroy": (None, [C.c_void_p]),
     "cfd_sched_step": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -75,7 +75,15 @@ struct cfd_unet {
     uint16_t* arena_thi = nullptr;  // split compute: f16 hi / lo parts of the scaled input-gradient packs
     uint16_t* arena_tlo = nullptr;
     int compute = CFD_COMPUTE_SPLIT_F16;
+    int tape_mode = CFD_TAPE_INPUT_VJP;   // what the next forward_tape records
+    int tape_mode_rec = CFD_TAPE_INPUT_VJP;   // what the last forward_tape recorded (the replays' layout)
     int* nonfinite = nullptr;  // range guard flag: set by the last convolution on a non-finite eps
+    // side stream of the forward (CFD_UNET_SIDE): the skip 1x1 convolutions and the
+    // timestep-embedding MLP, which depend on nothing the main stream computes next,
+    // run beside it and join before their consumer (event fork / join: captured
+    // into the samplers' HIP graphs as parallel branches)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     mutable std::map<int, size_t> ws_cache;  // workspace bytes per B (the dry walk is host work)
     uint64_t version = 0;   // bumped by every set_param / set_compute: launch arguments (weight
                             // scales, kernel choice) captured into a graph are stale after it
@@ -328,6 +336,8 @@ struct Rec {
 struct Tape {
     Workspace* tws;
     std::vector<Rec>* recs;
+    // CFD_TAPE_PARAM_GRAD: also keep the GroupNorm(+SiLU) outputs and their ranges
+    bool keep_gnout = false;
     // the timestep-embedding MLP's activations (kept for the parameter gradients):
     // timestep_embedding (B, mc), time_embed.0 output (B, tdim), emb (B, tdim)
     float* temb = nullptr;
@@ -404,6 +414,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     // normalised (+SiLU) input of the next conv (widest: an output block's concat)
     float* nbuf = ws.take((size_t)B * z.max_cat);
     float* splitk = ws.take(kSplitCap);
+    float* splitk_side = ws.take(kSplitCap);   // the side stream's split-K slab (skip convolutions)
     float* kvws = ws.take((size_t)B * z.max_kvf);
     float* pool[3];
     for (auto& p : pool) p = ws.take((size_t)B * z.max_act);
@@ -419,7 +430,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     int ngs = 0;
     if (ws.dry && !tape) return;
     auto keep = [&](size_t nfloats) -> float* { return tape->tws->take(nfloats); };
-    if (tape && launch) CFD_HIP(hipMemsetAsync(gslots, 0, sizeof(unsigned) * kGnSlots, st));
+    if (tape && tape->keep_gnout && launch) CFD_HIP(hipMemsetAsync(gslots, 0, sizeof(unsigned) * kGnSlots, st));
     std::vector<Rec>* recs = tape ? tape->recs : nullptr;
     if (recs) recs->assign(h->steps.size(), Rec{});
 
@@ -430,13 +441,37 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         throw cfd::Error{CFD_ESTATE, "internal: buffer pool exhausted"};
     };
 
-    // timestep embedding + time_embed MLP + every ResBlock's emb_layers (nn.py:118-136, unet.py:648,199-205)
+    // the side stream (CFD_UNET_SIDE=0: everything on st).  join_pending: the main
+    // stream must wait for the side stream before the next consumer of its result
+    static const int side_env = getenv("CFD_UNET_SIDE") ? atoi(getenv("CFD_UNET_SIDE")) : 1;
+    const bool use_side = side_env && launch && h->side;
+    bool join_pending = false;
+    auto fork = [&]() {
+        CFD_HIP(hipEventRecord(h->ev_fork, st));
+        CFD_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    };
+    auto join_mark = [&]() {
+        CFD_HIP(hipEventRecord(h->ev_join, h->side));
+        join_pending = true;
+    };
+    auto join = [&]() {
+        if (!join_pending) return;
+        CFD_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
+        join_pending = false;
+    };
+
+    // timestep embedding + time_embed MLP + every ResBlock's emb_layers (nn.py:118-136,
+    // unet.py:648,199-205): on the side stream, beside conv_in and the first GroupNorm;
+    // joined before the first convolution that adds emb
     if (launch) {
-        cfd::launch_temb(t, h->freqs, temb, mc, B, st);
-        cfd::launch_linear(temb, P(h, "time_embed.0.weight"), P(h, "time_embed.0.bias"), h1, B, mc, h->tdim, 0, st);
+        const hipStream_t es = use_side ? h->side : st;
+        if (use_side) fork();
+        cfd::launch_temb(t, h->freqs, temb, mc, B, es);
+        cfd::launch_linear(temb, P(h, "time_embed.0.weight"), P(h, "time_embed.0.bias"), h1, B, mc, h->tdim, 0, es);
         cfd::launch_linear(h1, P(h, "time_embed.2.weight"), P(h, "time_embed.2.bias"), emb, B, h->tdim, h->tdim, 1,
-                           st);
-        cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, st);
+                           es);
+        cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, es);
+        if (use_side) join_mark();
     }
 
     // A split-K convolution's reduction is deferred to its consumer: the
@@ -472,9 +507,10 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             *stats = g.stats = keep((size_t)B * 64);
         }
         g.out = nbuf;
-        // CFD_TAPE_GNOUT=0: the weight gradients recompute the activated input instead
+        // CFD_TAPE_PARAM_GRAD tapes keep it (CFD_TAPE_GNOUT=0 overrides: the weight
+        // gradients then recompute the activated input)
         static const int tape_gnout = getenv("CFD_TAPE_GNOUT") ? atoi(getenv("CFD_TAPE_GNOUT")) : 1;
-        if (tape && actp && tape_gnout) {   // kept for the weight gradients, with its range
+        if (tape && actp && tape_gnout && tape->keep_gnout) {   // kept for the weight gradients, with its range
             CFD_REQUIRE(!bf16_out && ngs < kGnSlots, CFD_ESTATE, "internal: kept GroupNorm output");
             g.out = keep((size_t)B * in.H * in.W * in.C());
             g.amax_out = gslots + ngs++;
@@ -640,7 +676,22 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 // convolution), so that in_layers' deferred reduction meets the
                 // out_layers GroupNorm directly   (unet.py:255-256)
                 const float* resp;
-                if (r.cin != r.cout) {
+                bool skip_side = false;
+                if (r.cin != r.cout && use_side) {
+                    // on the side stream, beside in_layers and the out_layers GroupNorm:
+                    // it reads only the block input (reduced by the GroupNorm above), its
+                    // own split-K slab, and reduces there (no deferral)
+                    join();          // the previous side work (emb) is consumed first
+                    flush();
+                    fork();
+                    cfd::ConvArgs a = conv_args(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
+                    a.part = splitk_side;
+                    const cfd::ConvPlan plan = plan_checked(a, kSplitCap);
+                    cfd::launch_conv(a, plan, h->side, /*defer=*/false);
+                    join_mark();
+                    skip_side = true;
+                    resp = skipb;
+                } else if (r.cin != r.cout) {
                     conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
                     resp = skipb;
                 } else {
@@ -648,12 +699,14 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     resp = cur.a;
                 }
                 float* hb = tape ? keep(nout) : tmp;
+                if (!skip_side) join();   // emb (the side stream's first work) before its first consumer
                 conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, hb);
                 rec.h1 = hb;
                 const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
                 const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2, /*keep_raw=*/tape != nullptr,
                                   feeds_k1hb(th, r.pre + ".out_layers.3", r.cout), &rec.act2, &rec.amx2);
                 float* out = dest(cur.a, cur.b, nout);
+                if (skip_side) join();
                 conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};
                 break;
@@ -723,6 +776,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         if (recs) (*recs)[si] = rec;
     }
     flush();
+    join();
 }
 
 
@@ -1131,6 +1185,9 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             CFD_HIP(hipMalloc(&h->freqs, sizeof(float) * std::max(half, 1)));
             CFD_HIP(hipMalloc(&h->nonfinite, sizeof(int)));
             CFD_HIP(hipMemset(h->nonfinite, 0, sizeof(int)));
+            CFD_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+            CFD_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+            CFD_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
             CFD_HIP(hipMemcpy(h->freqs, fr.data(), sizeof(float) * half, hipMemcpyHostToDevice));
         } catch (...) {
             cfd_unet_destroy(h);
@@ -1158,6 +1215,9 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->rp_part);
     (void)hipFree(h->rp_amax);
     (void)hipFree(h->rp_tfirst);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->side) (void)hipStreamDestroy(h->side);
     delete h;
 }
 
@@ -1659,13 +1719,29 @@ extern "C" int cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, f
     });
 }
 
+namespace {
+// tape bytes of a forward recorded in `mode`
+size_t tape_bytes_mode(const cfd_unet* h, int B, int mode) {
+    Workspace ws{nullptr, 0, true}, tws{nullptr, 0, true};
+    Tape tape{&tws, nullptr};
+    tape.keep_gnout = mode == CFD_TAPE_PARAM_GRAD;
+    run(h, nullptr, nullptr, nullptr, B, ws, nullptr, &tape, false);
+    return tws.off + 256;
+}
+}  // namespace
+
 extern "C" int cfd_unet_tape_bytes(const cfd_unet* h, int B, size_t* bytes) {
     return cfd::guard([&] {
         CFD_REQUIRE(h && bytes && B > 0, CFD_EARG, "bad argument");
-        Workspace ws{nullptr, 0, true}, tws{nullptr, 0, true};
-        Tape tape{&tws, nullptr};
-        run(h, nullptr, nullptr, nullptr, B, ws, nullptr, &tape, false);
-        *bytes = tws.off + 256;
+        *bytes = tape_bytes_mode(h, B, h->tape_mode);
+    });
+}
+
+extern "C" int cfd_unet_set_tape_mode(cfd_unet* h, int mode) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h, CFD_EARG, "null handle");
+        CFD_REQUIRE(mode == CFD_TAPE_INPUT_VJP || mode == CFD_TAPE_PARAM_GRAD, CFD_EARG, "unknown tape mode");
+        h->tape_mode = mode;
     });
 }
 
@@ -1696,13 +1772,14 @@ extern "C" int cfd_unet_forward_tape(cfd_unet* h, const float* x, const int64_t*
                     "or CFD_COMPUTE_SPLIT_F16 first");
         CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
         check_ready(h);
-        size_t need = 0, tneed = 0;
+        size_t need = 0;
         cfd_unet_workspace_bytes(h, B, &need);
-        cfd_unet_tape_bytes(h, B, &tneed);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        CFD_REQUIRE(tape_bytes >= tneed, CFD_EARG, "tape too small");
+        CFD_REQUIRE(tape_bytes >= tape_bytes_mode(h, B, h->tape_mode), CFD_EARG, "tape too small");
         Workspace ws{align256(workspace), 0, false}, tws{align256(tape), 0, false};
         Tape tp{&tws, nullptr};
+        tp.keep_gnout = h->tape_mode == CFD_TAPE_PARAM_GRAD;
+        h->tape_mode_rec = h->tape_mode;
         run(h, x, t, eps, B, ws, (hipStream_t)stream, &tp, true);
     });
 }
@@ -1713,16 +1790,16 @@ extern "C" int cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, i
         CFD_REQUIRE(h && d_eps && d_x && tape && workspace, CFD_EARG, "null argument");
         CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
         check_ready(h);
-        size_t need = 0, tneed = 0;
+        size_t need = 0;
         cfd_unet_vjp_workspace_bytes(h, B, &need);
-        cfd_unet_tape_bytes(h, B, &tneed);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        CFD_REQUIRE(tape_bytes >= tneed, CFD_EARG, "tape too small");
+        CFD_REQUIRE(tape_bytes >= tape_bytes_mode(h, B, h->tape_mode_rec), CFD_EARG, "tape too small");
         // replay the forward walk (no launches) over the same tape layout to
         // recover where every saved activation lives
         Workspace fws{nullptr, 0, true}, tws{align256(const_cast<void*>(tape)), 0, false};
         std::vector<Rec> recs;
         Tape tp{&tws, &recs};
+        tp.keep_gnout = h->tape_mode_rec == CFD_TAPE_PARAM_GRAD;
         run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
         Workspace ws{align256(workspace), 0, false};
         run_vjp(h, d_eps, d_x, B, recs, ws, (hipStream_t)stream);
@@ -1745,14 +1822,14 @@ extern "C" int cfd_unet_param_grad(cfd_unet* h, const float* x, const float* d_e
         CFD_REQUIRE(h && x && d_eps && tape && grad && workspace, CFD_EARG, "null argument");
         CFD_REQUIRE(B > 0, CFD_EARG, "B must be positive");
         check_ready(h);
-        size_t need = 0, tneed = 0;
+        size_t need = 0;
         cfd_unet_param_grad_workspace_bytes(h, B, &need);
-        cfd_unet_tape_bytes(h, B, &tneed);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        CFD_REQUIRE(tape_bytes >= tneed, CFD_EARG, "tape too small");
+        CFD_REQUIRE(tape_bytes >= tape_bytes_mode(h, B, h->tape_mode_rec), CFD_EARG, "tape too small");
         Workspace fws{nullptr, 0, true}, tws{align256(const_cast<void*>(tape)), 0, false};
         std::vector<Rec> recs;
         Tape tp{&tws, &recs};
+        tp.keep_gnout = h->tape_mode_rec == CFD_TAPE_PARAM_GRAD;
         run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
         ParamGrad pg;
         pg.grad = grad;

@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
             for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
         }
         gn_store4(a, pix * a.Ctot + c0, v);
-        mx = amax4(v);
+        mx = fmaxf(mx, amax4(v));   // every quad of the grid-stride loop, not the last
     }
     if (a.amax_out) block_amax_atomic(mx, a.amax_out);
 }

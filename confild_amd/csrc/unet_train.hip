@@ -258,13 +258,17 @@ __device__ __forceinline__ void wg_split4(f4 x, float s, uint2& hi, uint2& lo) {
     asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.y) : "v"(x[2]), "v"(hi.y));
     asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.y) : "v"(x[3]), "v"(hi.y));
 }
-// power of two s with max * s in [0.5, 1) (1 for an all-zero tensor)
+// power of two s with max * s in [2^14, 2^15) (1 for an all-zero tensor): the top
+// of the f16 range, so the bulk of a heavy-tailed operand stays above the f16
+// normal limit (2^-14) down to 2^-28 of its maximum -- hi.hi products reach 2^30
+// and fp32 sums over P < 2^24 pixels 2^54, far inside fp32.  The exponent is
+// clamped so s and 1/s stay normal (a tensor below 2^-111 keeps s = 2^126).
 __device__ __forceinline__ float wg_scale(unsigned amax_bits) {
     const float m = __uint_as_float(amax_bits);
     if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
     int e;
     (void)frexpf(m, &e);
-    return ldexpf(1.f, -e);
+    return ldexpf(1.f, min(15 - e, 126));
 }
 
 // max |x| over n floats (n % 4 == 0) into *out (atomicMax of the float bits)
@@ -421,7 +425,10 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
             for (int e = 0; e < 4; ++e)
                 if (m0 + 4 * q + e < M) a.bpart[(int64_t)blockIdx.z * M + m0 + 4 * q + e] = bsum[e];
     }
-    const float unscale = 1.f / (sx * sy);   // exact: a power of two
+    // 1/s_x and 1/s_y applied one after the other (each exact, a power of two in
+    // the normal range): their product could leave the fp32 range where s_x s_y
+    // does, and a flushed unscale would zero the gradient
+    const float usx = 1.f / sx, usy = 1.f / sy;
     float* Cz = a.part + (int64_t)blockIdx.z * M * N;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -431,7 +438,7 @@ __global__ __launch_bounds__(256) void conv_wgrad128_split_kernel(WgradArgs a, c
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = m0 + wm * 64 + 16 * i + 4 * g + r;
-                if (m < M) Cz[(int64_t)m * N + n] = acc[i][j][r] * unscale;
+                if (m < M) Cz[(int64_t)m * N + n] = (acc[i][j][r] * usx) * usy;
             }
         }
 }
@@ -531,7 +538,10 @@ __global__ __launch_bounds__(1024) void conv_wgrad_thin_kernel(WgradArgs a) {
 #pragma unroll
                 for (int t = 0; t < 9; ++t) acc[n][t] = fmaf(wv[u], nv[u][n][t], acc[n][t]);
     }
-    // the 16 pixel lanes' sums, added in lane order
+    // the 16 pixel lanes' sums, added in lane order.  NN = 4 makes this 144 KiB of
+    // static LDS: it fits gfx950's 160 KiB per workgroup only (the library is built
+    // for gfx950 alone; an older target's 64 KiB would fail to compile here)
+    static_assert(sizeof(float) * NPL * 64 * NN * 9 <= 160 * 1024, "thin wgrad: LDS beyond gfx950's 160 KiB");
     __shared__ float red[NPL][64][NN * 9];
 #pragma unroll
     for (int n = 0; n < NN; ++n)

@@ -469,7 +469,7 @@ class GaussianDiffusion:
         x_t = self.q_sample(x_start, t, noise=noise)
         tm = self._map_timesteps(t.to(device=x_t.device))
         with torch.no_grad():
-            out = model.forward_tape(x_t, tm) if grad is not None else model(x_t, tm)
+            out = model.forward_tape(x_t, tm, for_param_grad=True) if grad is not None else model(x_t, tm)
         target = noise if self.model_mean_type == ModelMeanType.EPSILON else x_start
         target = target.detach().to(torch.float32).contiguous()
         if out.shape != target.shape:

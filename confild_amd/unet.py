@@ -397,8 +397,10 @@ class UNetModel(nn.Module):
                        "cfd_unet_check_finite")
 
     # -- input-gradient (DPS adjoint) ---------------------------------------------
-    def forward_tape(self, x: torch.Tensor, timesteps: torch.Tensor) -> torch.Tensor:
-        """forward() that also records the activations for input_vjp (bit-identical eps)."""
+    def forward_tape(self, x: torch.Tensor, timesteps: torch.Tensor, for_param_grad: bool = False) -> torch.Tensor:
+        """forward() that also records the activations for input_vjp (bit-identical eps).
+        ``for_param_grad``: also keep the GroupNorm outputs param_grad's weight
+        gradients read (CFD_TAPE_PARAM_GRAD: more tape, a faster param_grad)."""
         x, t, B = self._prep(x, timesteps)
         if self.compute == "bf16":
             raise NotImplementedError("the input-gradient (DPS) path is fp32-accurate: set_compute('fp32') or "
@@ -406,6 +408,9 @@ class UNetModel(nn.Module):
         h = self._handle(x.device)
         lib = _lib.load()
         ws = self._workspace(h, x.device, B)
+        mode = 1 if for_param_grad else 0   # CFD_TAPE_PARAM_GRAD / CFD_TAPE_INPUT_VJP
+        _lib.check(lib.cfd_unet_set_tape_mode(h, mode), "cfd_unet_set_tape_mode")
+        self._tape_mode = mode
         tape = self._tape_buf(h, x.device, B)
         eps = torch.empty((B, self.out_channels, self.image_size, self.image_size), dtype=torch.float32,
                           device=x.device)
@@ -525,7 +530,8 @@ class UNetModel(nn.Module):
         return grad
 
     def _tape_buf(self, h, device, B):
-        key = (device, B)
+        # sized for the mode of the last forward_tape (input_vjp / param_grad replay it)
+        key = (device, B, getattr(self, "_tape_mode", 0))
         if getattr(self, "_tape_key", None) != key:
             n = C.c_size_t()
             _lib.check(_lib.load().cfd_unet_tape_bytes(h, B, C.byref(n)), "tape bytes")

@@ -122,6 +122,16 @@ int  cfd_unet_forward_tape(cfd_unet* h, const float* x, const int64_t* t, float*
                            void* workspace, size_t ws_bytes, void* tape, size_t tape_bytes, void* stream);
 int  cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, int B, const void* tape,
                         size_t tape_bytes, void* workspace, size_t ws_bytes, void* stream);
+/* What the next cfd_unet_forward_tape records (and cfd_unet_tape_bytes sizes):
+ * CFD_TAPE_INPUT_VJP (default) the activations cfd_unet_input_vjp reads, nothing
+ * more (the DPS adjoint); CFD_TAPE_PARAM_GRAD also every GroupNorm(+SiLU) output
+ * the convolutions read and its max |.| -- the operands of cfd_unet_param_grad's
+ * split weight gradients, which otherwise recompute them (one activation per
+ * GroupNorm of tape memory, +0.3 ms per Case1 forward, -2.5 ms per backward).
+ * input_vjp / param_grad replay the layout of the mode the tape was recorded in. */
+#define CFD_TAPE_INPUT_VJP  0
+#define CFD_TAPE_PARAM_GRAD 1
+int  cfd_unet_set_tape_mode(cfd_unet* h, int mode);
 
 /* ------------------------------------------------------------------------ */
 /* Diffusion step epilogue (replaces p_mean_variance + p_sample / ddim_sample */

@@ -78,16 +78,26 @@ def test_unet_param_grad_matches_autograd(hip, name):
     assert errs[0][0] < 2e-4, errs[:8]
 
 
-def test_unet_param_grad_split_is_fp32_level(hip):
+@pytest.mark.parametrize("tail", ["normal", "outliers"])
+@pytest.mark.parametrize("kept", [False, True])
+def test_unet_param_grad_split_is_fp32_level(hip, tail, kept):
     """Split-f16 weight-gradient products (split compute, the default; every
     convolution of wide128 runs them): each gradient tensor's error against a
     float64 autograd evaluation stays within 2x the fp32 mode's (exact fp32-MFMA
     products) + 1e-7 of the model's largest gradient -- the criterion the split
-    forward and input-gradient meet (test_gpu_unet_split.py, test_gpu_dps.py)."""
+    forward and input-gradient meet (test_gpu_unet_split.py, test_gpu_dps.py).
+    ``kept``: the CFD_TAPE_PARAM_GRAD tape (GroupNorm outputs and their ranges
+    kept by the forward) or the input-VJP tape (the operands recomputed).
+    ``outliers``: a heavy-tailed d_eps (eight pixels 1e4x the rest), so every
+    backward tensor's bulk sits far below its maximum -- the operand scaling must
+    keep the bulk's hi / lo halves in the f16 normal range."""
     g, cfg, sd, m = _unet("wide128")
     x = torch.from_numpy(g["x"])
     t = torch.from_numpy(g["t"])
     d_eps = torch.from_numpy(synth.normal(5, "wide128/deps", tuple(x.shape)))
+    if tail == "outliers":
+        flat_idx = torch.from_numpy(synth.normal(6, "wide128/outl", (8,))).abs().mul(997).long() % d_eps.numel()
+        d_eps.view(-1)[flat_idx] *= 1e4
     params = {k: v.double().requires_grad_(True) for k, v in sd.items()}
     eps_ref = ou.forward(params, cfg, x.double(), t)
     ref = dict(zip(params.keys(), torch.autograd.grad(eps_ref, list(params.values()), d_eps.double())))
@@ -96,7 +106,7 @@ def test_unet_param_grad_split_is_fp32_level(hip):
     err = {}
     for mode in ("fp32", "split_f16"):
         m.set_compute(mode)
-        m.forward_tape(x.to(DEV), t.to(DEV))
+        m.forward_tape(x.to(DEV), t.to(DEV), for_param_grad=kept)
         flat = m.param_grad(d_eps.to(DEV)).cpu().double()
         o, e = 0, {}
         for k in m.param_keys():
@@ -108,6 +118,45 @@ def test_unet_param_grad_split_is_fp32_level(hip):
     print(f"wide128 split vs fp32 gradient error (excess over 2x fp32, / max grad {gmax:.3e}): {worst}")
     for k in err["fp32"]:
         assert err["split_f16"][k] <= 2 * err["fp32"][k] + 1e-7 * gmax, (k, err["split_f16"][k], err["fp32"][k])
+
+
+def test_unet_param_grad_split_large_groupnorm(hip):
+    """The GroupNorms of a 128^2 x 256-channel level run the three-kernel path
+    (gn_partial / gn_finalize / gn_apply) and gn_apply's bounded grid-stride loop
+    covers > 4096 x 256 float4 quads per workgroup grid (B = 4: 4.2 M), so each
+    thread handles several quads.  The range slot each kept output carries (the
+    split weight gradients' operand scale) must be the max over all of them: split
+    and fp32 parameter gradients agree to fp32 level, with the kept-output tape
+    and with the recomputed operands alike (an underestimated range overflows the
+    f16 halves)."""
+    kw = {"image_size": 128, "num_channels": 128, "num_res_blocks": 1, "channel_mult": "2,2", "num_heads": 4,
+          "num_head_channels": 64, "attention_resolutions": "16"}
+    m = create_model(**kw)
+    sd = synth.unet_state_dict(41, {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.to(DEV)
+    x = torch.from_numpy(synth.normal(42, "gnbig/x", (4, 1, 128, 128))).to(DEV)
+    t = torch.tensor([3, 250, 600, 990], dtype=torch.int64, device=DEV)
+    d = torch.from_numpy(synth.normal(43, "gnbig/d", (4, 1, 128, 128))).to(DEV)
+    grads = {}
+    for mode, kept in (("fp32", True), ("split_f16", True), ("split_f16", False)):
+        m.set_compute(mode)
+        m.forward_tape(x, t, for_param_grad=kept)
+        grads[(mode, kept)] = m.param_grad(d).cpu()
+    named = dict(m.named_parameters())
+    ref = grads[("fp32", True)]
+    gmax = float(ref.abs().max())
+    for key in (("split_f16", True), ("split_f16", False)):
+        got, o, worst = grads[key], 0, (0.0, "")
+        assert torch.isfinite(got).all(), key
+        for k in m.param_keys():
+            n = named[k].numel()
+            r, gk = ref[o:o + n], got[o:o + n]
+            o += n
+            e = float((gk - r).abs().max()) / max(float(r.abs().max()), 1e-3 * gmax)
+            worst = max(worst, (e, k))
+        print(f"128^2 x 256ch B=4, split vs fp32 parameter gradients, {key}: worst {worst}")
+        assert worst[0] < 2e-4, (key, worst)
 
 
 def test_unet_param_grad_accumulates_and_is_deterministic(hip):
