@@ -49,7 +49,10 @@ __device__ __forceinline__ void split4_mix_x(const f4& x, uint2& hi, uint2& lo) 
 // PF: tiles in flight through registers (1: the next tile; 2: two ahead, two
 // register sets -- for short per-workgroup K ranges where one tile of compute
 // does not cover a load's latency).
-template <int BM, int BN, int WGM, int WGN, int KG, int PF = 1>
+// XF: a fused 1x1 skip convolution (ConvArgs::xsrc1): K tiles past the 3x3 taps'
+// (the "tap" ks * ks) take the raw block input at the output pixel and the skip
+// weights -- [taps | x] as one GEMM, in the same split-K ranges
+template <int BM, int BN, int WGM, int WGN, int KG, int PF = 1, bool XF = false>
 __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs a) {
     constexpr int NW = WGM * WGN * KG, NT = 64 * NW;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
@@ -79,11 +82,24 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));   // SGPR: a VGPR descriptor field costs a readfirstlane loop per load
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
+        (void*)(a.src2 ? (const void*)a.src2 : (const void*)a.src1), 0, a.src2 ? srows * a.C2 * 4 : 0, 0x00020000);
+    const int ntap = a.ks * a.ks, KM = ntap * a.Ctot;   // the taps' K (XF: the skip part follows)
+    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * KM * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * KM * 2, 0x00020000);
+    __amdgpu_buffer_rsrc_t rx1 = rs1, rx2 = rs1, rxh = rwh, rxl = rwl;
+    // the skip part's fields as locals: a select between two fields of `a` would
+    // take the kernel argument's address and copy it to scratch
+    const int XC1 = a.XC1, XC2 = a.XC2;
+    const float xscale = a.x_scale, mscale = a.main_scale;
+    if constexpr (XF) {
+        const int XC = XC1 + XC2, mrows = __builtin_amdgcn_readfirstlane(a.M);
+        rx1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.xsrc1, 0, mrows * a.XC1 * 4, 0x00020000);
+        rx2 = __builtin_amdgcn_make_buffer_rsrc((void*)(a.xsrc2 ? (const void*)a.xsrc2 : (const void*)a.xsrc1), 0,
+                                                a.xsrc2 ? mrows * a.XC2 * 4 : 0, 0x00020000);
+        rxh = __builtin_amdgcn_make_buffer_rsrc((void*)a.xwbf, 0, a.Cout * XC * 2, 0x00020000);
+        rxl = __builtin_amdgcn_make_buffer_rsrc((void*)a.xwlo, 0, a.Cout * XC * 2, 0x00020000);
+    }
     {
-        const int ntap = a.ks * a.ks;
         const float rhw = 1.0f / (float)HWo, rw = 1.0f / (float)a.Wout;   // fdiv24 (M < 2^24: launch_conv_x)
         for (int e = tid; e < ntap * BM; e += NT) {
             const int tap = e / BM, r = e - tap * BM;
@@ -123,14 +139,15 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
         a_m[it] = rs % BM;
     }
     int b_g[BIT], b_row[BIT];
-    unsigned b_voff[BIT];
+    unsigned b_voff[BIT], bx_voff[BIT];
 #pragma unroll
     for (int it = 0; it < BIT; ++it) {
         const int rs = rsub + it * RPP;
         b_g[it] = rs / BN;
         b_row[it] = rs;
         const int n = n0 + rs % BN;
-        b_voff[it] = n < a.Cout ? (unsigned)((n * a.K + 4 * kq) * 2) : 0x80000000u;
+        b_voff[it] = n < a.Cout ? (unsigned)((n * KM + 4 * kq) * 2) : 0x80000000u;
+        bx_voff[it] = XF && n < a.Cout ? (unsigned)((n * (a.XC1 + a.XC2) + 4 * kq) * 2) : 0x80000000u;
     }
 
     const int nkt = a.K / 32;
@@ -142,48 +159,74 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 #pragma unroll
     for (int g = 0; g < KG; ++g) {
         const int kb = (kt0 + g) * 32;
-        tpg[g] = __builtin_amdgcn_readfirstlane(kb / a.Ctot);   // SGPRs: scalar descriptor choice
-        cbg[g] = __builtin_amdgcn_readfirstlane(kb - tpg[g] * a.Ctot);
+        // tap ntap (XF): the skip part, channel kb - KM of the block input
+        const int tp = XF && kb >= KM ? ntap : kb / a.Ctot;
+        tpg[g] = __builtin_amdgcn_readfirstlane(tp);   // SGPRs: scalar descriptor choice
+        cbg[g] = __builtin_amdgcn_readfirstlane(kb - tp * a.Ctot);
     }
     __syncthreads();   // pixtab
 
     f4 ra[PF][AIT];
     uint2 rbh[PF][BIT], rbl[PF][BIT];
-    auto load_tile = [&](int kt, int set) {   // tiles kt + g, g < KG, into register set `set`
+    float lsc[PF][KG];   // XF: the staging scale of each group's tile (main_scale / x_scale)
+    auto load_tile = [&](int kt, int set) __attribute__((always_inline)) {   // tiles kt + g, g < KG, into register set `set`
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
-            const int g = a_g[it];
+            const int g = KG == 1 ? 0 : a_g[it];   // KG = 1: a constant (a runtime index puts tpg / cbg in scratch)
             const int cb = cbg[g];
+            bool xt = false;
+            if constexpr (XF) xt = tpg[g] == ntap;
+            if (xt) {   // the skip part (XF): the block input at the output pixel itself
+                const bool second = cb >= XC1;
+                const unsigned csrc4 = 4u * (second ? XC2 : XC1);
+                const unsigned cofs4 = 4u * ((second ? cb - XC1 : cb) + 4 * kq);
+                const int m = m0 + a_m[it];
+                const unsigned off = kt + g < kt1 && m < a.M ? __umul24((unsigned)m, csrc4) + cofs4 : 0x80000000u;
+                ra[set][it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(second ? rx2 : rx1, off, 0, 0));
+            } else {
             const bool second = cb >= a.C1;
             const unsigned csrc4 = 4u * (second ? a.C2 : a.C1);
             const unsigned cofs4 = 4u * ((second ? cb - a.C1 : cb) + 4 * kq);
             const int pix = kt + g < kt1 ? pixtab[tpg[g] * BM + a_m[it]] : -1;
             const unsigned off = pix >= 0 ? __umul24((unsigned)pix, csrc4) + cofs4 : 0x80000000u;
             ra[set][it] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(second ? rs2 : rs1, off, 0, 0));
+            }
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
-            const int g = b_g[it];
-            const unsigned voff = kt + g < kt1 ? b_voff[it] : 0x80000000u;
-            const int soff = (tpg[g] * a.Ctot + cbg[g]) * 2;
-            rbh[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, voff, soff, 0));
-            rbl[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, voff, soff, 0));
+            const int g = KG == 1 ? 0 : b_g[it];
+            bool xt = false;
+            if constexpr (XF) xt = tpg[g] == ntap;
+            if (xt) {
+                const unsigned voff = kt + g < kt1 ? bx_voff[it] : 0x80000000u;
+                rbh[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rxh, voff, cbg[g] * 2, 0));
+                rbl[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rxl, voff, cbg[g] * 2, 0));
+            } else {
+                const unsigned voff = kt + g < kt1 ? b_voff[it] : 0x80000000u;
+                const int soff = (tpg[g] * a.Ctot + cbg[g]) * 2;
+                rbh[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, voff, soff, 0));
+                rbl[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, voff, soff, 0));
+            }
         }
 #pragma unroll
         for (int g = 0; g < KG; ++g) {
+            if constexpr (XF) lsc[set][g] = tpg[g] == ntap ? xscale : mscale;
             cbg[g] += 32 * KG;
-            while (cbg[g] >= a.Ctot) {
+            while (cbg[g] >= a.Ctot && tpg[g] < ntap) {   // past the last tap: the skip part (XF)
                 cbg[g] -= a.Ctot;
                 ++tpg[g];
             }
         }
     };
-    auto store_tile = [&](int buf, int set) {
+    auto store_tile = [&](int buf, int set) __attribute__((always_inline)) {
         char* base = lds + buf * STAGE;
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
             uint2 hv, lv;
-            split4_mix_x(ra[set][it], hv, lv);
+            if constexpr (XF)
+                split4_mix_x(ra[set][it] * lsc[set][KG == 1 ? 0 : a_g[it]], hv, lv);   // the common scale (exact)
+            else
+                split4_mix_x(ra[set][it], hv, lv);
             const int off = xswz(a_row[it], kq >> 1) + (kq & 1) * 8;
             *(uint2*)(base + off) = hv;
             *(uint2*)(base + ABYTES + off) = lv;
@@ -209,7 +252,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     // one K step (tiles kt + g): prefetch the tiles PF steps ahead into register
     // set `lset`, MFMAs on LDS stage `cur`, then stage the next step's tiles
     // (register set `sset`, loaded PF - 1 steps ago) into the other LDS stage
-    auto kstep = [&](int kt, int cur, int lset, int sset) {
+    auto kstep = [&](int kt, int cur, int lset, int sset) __attribute__((always_inline)) {
             const bool more = kt + KG < kt1;
             if (kt + PF * KG < kt1) load_tile(kt + PF * KG, lset);
             const char* base = lds + cur * STAGE;
@@ -340,6 +383,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
                 const int n = n_base + 32 * j;
                 if (n >= a.Cout) continue;
                 float v = a.bias ? acc[i][j][e] + a.bias[n] : acc[i][j][e];
+                if (XF && a.bias2) v = v + a.bias2[n];
                 if (a.emb) v = v + a.emb[(int64_t)bb * a.emb_stride + n];
                 if (a.res) v = a.res[(int64_t)m * a.Cout + n] + v;
                 a.out[(int64_t)m * a.Cout + n] = v;
@@ -388,9 +432,18 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 // batch twice the workgroups, one wave per SIMD -- the same tiles' sums)
 // OCC: waves per SIMD the register allocation must allow (launch bound) -- 4 lets
 // two 8-wave K1hb workgroups share a CU where the grid has more than one per CU
-template <int BM, int TW, int KG = 1, bool BF = false, bool SB = false, int BN = 128, int OCC = 1>
+// XF: a fused 1x1 skip convolution (ConvArgs::xsrc1, split compute, KG = 1): after
+// the halo rounds the workgroup runs one step per 32-channel chunk of the raw
+// block input, read at the tile's own pixels (no halo) into a double buffer of
+// its own, two chunks ahead in registers, against the skip weights in the same
+// ring -- the ResBlock's skip(x) + h as one GEMM over [h taps | x], no skip tensor
+// written or re-read and no launch of its own.  The split-K range of the X chunks
+// follows the halo chunks' (same split count); each output's summation order is
+// a function of the per-sample shape only.
+template <int BM, int TW, int KG = 1, bool BF = false, bool SB = false, int BN = 128, int OCC = 1, bool XF = false>
 __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvArgs a) {
     static_assert(!SB || BF, "a bf16 source needs the bf16 kernel");
+    static_assert(!XF || (KG == 1 && !BF), "fused skip convolution: split compute, one K group");
     constexpr unsigned SES = SB ? 2u : 4u;   // source element bytes
     constexpr int WGN = BN / 64, WGM = BM / 64, NTG = 64 * WGM * WGN;   // threads per K group (the workgroup: NTG * KG)
     static_assert(BN == 64 || BN == 128, "K1h: 64 or 128 output channels per workgroup");
@@ -406,7 +459,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     // 20 pixels apart) the chunk rotation also takes the row, (px/4 + 3 hr) mod 4, so
     // that the two rows' pixels of one ds_read_b128 lane group fall in different
     // bank slots (PMC: 0.24 LDS bank-conflict rate with xswz alone)
-    auto hswz = [](int px, int hr, int chunk) {
+    auto hswz = [](int px, int hr, int chunk) __attribute__((always_inline)) {
         if constexpr (TW == 16) return px * 64 + ((chunk ^ (((px >> 2) + 3 * hr) & 3)) << 4);
         else return xswz(px, chunk);
     };
@@ -417,7 +470,9 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     constexpr int GBYTES = PL * HPLANE + 2 * BSTAGE;  // one group's halo + weight ring
     static_assert(BM % TW == 0 && BIT >= 1, "tile");
     constexpr int RED = (KG - 1) * WGM * WGN * 4 * 16 * 64 * 4;   // parked sums of groups 1..
-    __shared__ __attribute__((aligned(16))) char lds[KG * GBYTES > RED ? KG * GBYTES : RED];
+    constexpr int LMAIN = KG * GBYTES > RED ? KG * GBYTES : RED;
+    constexpr int XBYTES = BM * 64 * 2;                            // one X chunk: hi + lo planes
+    __shared__ __attribute__((aligned(16))) char lds[LMAIN + (XF ? 2 * XBYTES : 0)];
 
     CFD_STAMP(a.stamps, 3, a.seq, 0);
     const int tid = threadIdx.x, lane = tid & 63;
@@ -442,9 +497,9 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     const int srows = __builtin_amdgcn_readfirstlane(a.Hin * a.Win * (a.M / HWo));
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.src1, 0, srows * a.C1 * SES, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.src2 ? a.src2 : a.src1), 0, a.src2 ? srows * a.C2 * SES : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * a.K * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * a.K * 2, 0x00020000);
+        (void*)(a.src2 ? (const void*)a.src2 : (const void*)a.src1), 0, a.src2 ? srows * a.C2 * SES : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wbf, 0, a.Cout * 9 * a.Ctot * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc((void*)a.wlo, 0, a.Cout * 9 * a.Ctot * 2, 0x00020000);
 
     // halo pieces of this thread: halo pixel (gt + it*NTG) >> 3, channel quad gt & 7
     const int kq = gt & 7;
@@ -468,7 +523,42 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
 #pragma unroll
     for (int it = 0; it < BIT; ++it) {
         const int n = n0 + (gt >> 2) + it * (NTG / 4);
-        bvoff[it] = n < a.Cout ? (unsigned)((n * a.K + 8 * bq) * 2) : 0x80000000u;
+        bvoff[it] = n < a.Cout ? (unsigned)((n * 9 * a.Ctot + 8 * bq) * 2) : 0x80000000u;
+    }
+
+    // fused skip convolution: this workgroup's X chunks [xc0, xc0 + nx) (the same
+    // split of the X channels as of the halo chunks), the tile pixels' offsets,
+    // the sources' and the skip weights' descriptors
+    constexpr int XIT = XF ? BM * 8 / NTG : 1;   // 16-B X pieces per thread and chunk
+    int nx = 0, xc0 = 0;
+    int xpix[XIT];
+    unsigned bxoff[BIT];
+    __amdgpu_buffer_rsrc_t rx1 = rs1, rx2 = rs1, rxh = rwh, rxl = rwl;
+    char* const xreg = lds + LMAIN;
+    // fields as locals (a select between two fields of `a` takes its address: a scratch copy)
+    const int XC1 = a.XC1, XC2 = a.XC2;
+    const float xscale = a.x_scale, mscale = a.main_scale;
+    if constexpr (XF) {
+        const int XC = a.XC1 + a.XC2, nxc = XC / 32;
+        const int xper = (nxc + gridDim.z - 1) / gridDim.z;
+        xc0 = bz * xper;
+        nx = max(0, min(nxc, xc0 + xper) - xc0);
+#pragma unroll
+        for (int it = 0; it < XIT; ++it) {
+            const int px = (gt + it * NTG) >> 3;
+            xpix[it] = (int)(mrow0 + (px / TW) * W + (px % TW));
+        }
+        const int mrows = __builtin_amdgcn_readfirstlane(a.M);
+        rx1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.xsrc1, 0, mrows * a.XC1 * 4, 0x00020000);
+        rx2 = __builtin_amdgcn_make_buffer_rsrc((void*)(a.xsrc2 ? (const void*)a.xsrc2 : (const void*)a.xsrc1), 0,
+                                                a.xsrc2 ? mrows * a.XC2 * 4 : 0, 0x00020000);
+        rxh = __builtin_amdgcn_make_buffer_rsrc((void*)a.xwbf, 0, a.Cout * XC * 2, 0x00020000);
+        rxl = __builtin_amdgcn_make_buffer_rsrc((void*)a.xwlo, 0, a.Cout * XC * 2, 0x00020000);
+#pragma unroll
+        for (int it = 0; it < BIT; ++it) {
+            const int n = n0 + (gt >> 2) + it * (NTG / 4);
+            bxoff[it] = n < a.Cout ? (unsigned)((n * XC + 8 * bq) * 2) : 0x80000000u;
+        }
     }
 
     // this workgroup's chunks [c0, c1); group kg takes the contiguous sub-range
@@ -481,16 +571,16 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     const int gper = (max(c1 - c0, 0) + KG - 1) / KG;
     const int cend = min(c1, c0 + (kg + 1) * gper);
     const int nrounds = gper;
-    auto chunk_of = [&](int r) { return c0 + kg * gper + r; };
+    auto chunk_of = [&](int r) __attribute__((always_inline)) { return c0 + kg * gper + r; };
 
     typedef typename std::conditional<SB, uint2, f4>::type HT;   // one halo piece in registers
     HT rh[HIT];
     u4 wx_h[BIT], wx_l[BIT], wy_h[BIT], wy_l[BIT];   // weight slices two steps deep
-    auto load_halo = [&](int c) {
+    auto load_halo = [&](int c) __attribute__((always_inline)) {
         const int cb = 32 * c;
         const bool second = cb >= a.C1;
-        const unsigned csrc = SES * (second ? a.C2 : a.C1);          // bytes per source pixel
-        const unsigned cofs = SES * ((second ? cb - a.C1 : cb) + 4 * kq);
+        const unsigned csrc = SES * (unsigned)(second ? a.C2 + 0 : a.C1 + 0);   // bytes per source pixel (a select
+        const unsigned cofs = SES * ((second ? cb - a.C1 : cb) + 4 * kq);      // of values: no argument copy)
         // one descriptor per branch (a selected descriptor would land in VGPRs)
         if (second) {
 #pragma unroll
@@ -512,7 +602,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
             }
         }
     };
-    auto store_halo = [&]() {
+    auto store_halo = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int it = 0; it < HIT; ++it) {
             const int e = gt + it * NTG;
@@ -524,15 +614,68 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                     *(bf16x4*)(halo + off) = __builtin_convertvector(rh[it], bf16x4);
                 } else {
                     uint2 hv, lv;
-                    split4_mix_x(rh[it], hv, lv);
+                    if constexpr (XF)
+                        split4_mix_x(rh[it] * mscale, hv, lv);   // the common scale (exact)
+                    else
+                        split4_mix_x(rh[it], hv, lv);
                     *(uint2*)(halo + off) = hv;
                     *(uint2*)(halo + HPLANE + off) = lv;
                 }
             }
         }
     };
-    // step s = (round s / 9, tap s % 9)
-    auto load_w = [&](int s, u4 (&rbh)[BIT], u4 (&rbl)[BIT]) {
+    const int NH = nrounds * 9;   // halo steps; the X steps follow
+    // X chunk j of this workgroup into a register set / from it into X buffer j & 1.
+    // Chunk j lives in the set of its step's parity ((NH + j) & 1: xr0 even, xr1 odd),
+    // picked by a uniform branch -- a runtime index into one array would put it in
+    // scratch
+    f4 xr0[XIT], xr1[XIT];
+    auto load_x = [&](int j, f4 (&dst)[XIT]) __attribute__((always_inline)) {
+        if constexpr (XF) {
+            const int cb = 32 * (xc0 + j);
+            const bool second = cb >= XC1;
+            const unsigned csrc = 4u * (unsigned)(second ? XC2 + 0 : XC1 + 0);   // prvalues: a select of values
+            const unsigned cofs = 4u * ((second ? cb - XC1 : cb) + 4 * kq);
+            if (second) {
+#pragma unroll
+                for (int it = 0; it < XIT; ++it)
+                    dst[it] = __builtin_bit_cast(
+                        f4, __builtin_amdgcn_raw_buffer_load_b128(rx2, __umul24((unsigned)xpix[it], csrc) + cofs, 0, 0));
+            } else {
+#pragma unroll
+                for (int it = 0; it < XIT; ++it)
+                    dst[it] = __builtin_bit_cast(
+                        f4, __builtin_amdgcn_raw_buffer_load_b128(rx1, __umul24((unsigned)xpix[it], csrc) + cofs, 0, 0));
+            }
+        }
+    };
+    auto store_x = [&](int j, const f4 (&src)[XIT]) __attribute__((always_inline)) {
+        if constexpr (XF) {
+            char* xb = xreg + (j & 1) * XBYTES;
+#pragma unroll
+            for (int it = 0; it < XIT; ++it) {
+                const int px = (gt + it * NTG) >> 3;
+                const int off = xswz(px, kq >> 1) + (kq & 1) * 8;
+                uint2 hv, lv;
+                split4_mix_x(src[it] * xscale, hv, lv);
+                *(uint2*)(xb + off) = hv;
+                *(uint2*)(xb + BM * 64 + off) = lv;
+            }
+        }
+    };
+    // step s = (round s / 9, tap s % 9); s >= NH: X chunk s - NH
+    auto load_w = [&](int s, u4 (&rbh)[BIT], u4 (&rbl)[BIT]) __attribute__((always_inline)) {
+        if constexpr (XF) {
+            if (s >= NH) {
+                const int soff = 64 * (xc0 + s - NH);
+#pragma unroll
+                for (int it = 0; it < BIT; ++it) {
+                    rbh[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rxh, bxoff[it], soff, 0));
+                    rbl[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rxl, bxoff[it], soff, 0));
+                }
+                return;
+            }
+        }
         const int c = chunk_of(s / 9), t = s % 9;
         if (c >= cend) return;
         const int soff = (t * a.Ctot + 32 * c) * 2;
@@ -543,7 +686,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                 rbl[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwl, bvoff[it], soff, 0));
         }
     };
-    auto store_w = [&](int stage, const u4 (&rbh)[BIT], const u4 (&rbl)[BIT]) {
+    auto store_w = [&](int stage, const u4 (&rbh)[BIT], const u4 (&rbl)[BIT]) __attribute__((always_inline)) {
         char* base = ring + stage * BSTAGE;
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
@@ -570,21 +713,38 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
         hrb[i] = p / TW;
     }
     const int brow0 = wn * 64 + l32;
-    const int nsteps = nrounds * 9;
+    const int nsteps = NH + nx;
 
     // one step: prefetch the weights of step s + 2, MFMAs of step s on ring stage
     // s & 1, then park step s + 1's weights (loaded a step ago) in the other
     // stage.  Every thread runs every step (the barriers are workgroup-wide); a
     // group whose chunk of the round is past the range only skips its work.
-    auto step = [&](int s, u4 (&ldh)[BIT], u4 (&ldl)[BIT], const u4 (&sth)[BIT], const u4 (&stl)[BIT]) {
-        const int r = s / 9, t = s - 9 * r;
+    // XF: steps s >= NH are X chunk j = s - NH (buffer j & 1, the ring's skip
+    // weights).  Chunk j lives in the register set of its step's parity: at this
+    // call site ldx is the set of s's parity (chunk j + 2 goes there), stx the other
+    // (chunk j + 1, parked into the other buffer at the end of the step) -- fixed
+    // per call site, so no runtime-selected register array (scratch)
+    auto step = [&](int s, u4 (&ldh)[BIT], u4 (&ldl)[BIT], const u4 (&sth)[BIT], const u4 (&stl)[BIT],
+                    f4 (&ldx)[XIT], f4 (&stx)[XIT]) __attribute__((always_inline)) {
+        const bool xs = XF && s >= NH;
+        const int r = s / 9, t = s - 9 * r, j = s - NH;
         const int c = chunk_of(r);
         if (s + 2 < nsteps) load_w(s + 2, ldh, ldl);
-        if (t == 0 && chunk_of(r + 1) < cend) load_halo(chunk_of(r + 1));   // in registers until this chunk's taps are done
-        if (c < cend) {
+        if (!xs && t == 0 && chunk_of(r + 1) < cend) load_halo(chunk_of(r + 1));   // in registers until this chunk's taps are done
+        if constexpr (XF) {
+            if (!xs && t == 0 && r + 1 == nrounds && nx > 0) {   // the last halo round: the first X chunks
+                load_x(0, stx);               // step NH has the parity opposite to s = NH - 9
+                if (nx > 1) load_x(1, ldx);
+            }
+            if (xs && j + 2 < nx) load_x(j + 2, ldx);
+        }
+        if (xs || c < cend) {
+            const char* wb = ring + (s & 1) * BSTAGE;
+            // A fragments: the halo at this tap, or the X buffer at the tile pixel
             const int ty = t / 3;
             const int tofs = ty * HW2 + (t - 3 * ty);
-            const char* wb = ring + (s & 1) * BSTAGE;
+            const char* ab = xs ? xreg + (j & 1) * XBYTES : halo;
+            const int aplane = xs ? BM * 64 : HPLANE;
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const int ch = 2 * s2 + hsel;
@@ -593,42 +753,48 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
 #pragma unroll
                     for (int i = 0; i < 2; ++i) fa[i] = *(const bf16x8*)(halo + hswz(hb[i] + tofs, hrb[i] + ty, ch));
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) fb[j] = *(const bf16x8*)(wb + xswz(brow0 + 32 * j, ch));
+                    for (int jj = 0; jj < 2; ++jj) fb[jj] = *(const bf16x8*)(wb + xswz(brow0 + 32 * jj, ch));
 #pragma unroll
                     for (int i = 0; i < 2; ++i)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                        for (int jj = 0; jj < 2; ++jj)
+                            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
                     continue;
                 }
                 h8v fah[2], fal[2], fbh[2], fbl[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    CFD_DASSERT(hb[i] + tofs < NPX);
-                    const int off = hswz(hb[i] + tofs, hrb[i] + ty, ch);
-                    fah[i] = *(const h8v*)(halo + off);
-                    fal[i] = *(const h8v*)(halo + HPLANE + off);
+                    CFD_DASSERT(xs || hb[i] + tofs < NPX);
+                    const int off = xs ? xswz(wm * 64 + 32 * i + l32, ch) : hswz(hb[i] + tofs, hrb[i] + ty, ch);
+                    fah[i] = *(const h8v*)(ab + off);
+                    fal[i] = *(const h8v*)(ab + aplane + off);
                 }
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int off = xswz(brow0 + 32 * j, ch);
-                    fbh[j] = *(const h8v*)(wb + off);
-                    fbl[j] = *(const h8v*)(wb + BPLANE + off);
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int off = xswz(brow0 + 32 * jj, ch);
+                    fbh[jj] = *(const h8v*)(wb + off);
+                    fbl[jj] = *(const h8v*)(wb + BPLANE + off);
                 }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                    for (int jj = 0; jj < 2; ++jj) {
+                        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[jj], acc[i][jj], 0, 0, 0);
+                        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[jj], acc[i][jj], 0, 0, 0);
+                        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[jj], acc[i][jj], 0, 0, 0);
                     }
             }
         }
-        if (s + 1 < nsteps && chunk_of((s + 1) / 9) < cend) store_w((s + 1) & 1, sth, stl);
+        if (s + 1 < nsteps && (s + 1 >= NH || chunk_of((s + 1) / 9) < cend)) store_w((s + 1) & 1, sth, stl);
+        if constexpr (XF) {
+            if (xs && j + 1 < nx) store_x(j + 1, stx);
+        }
         __syncthreads();
-        if (t == 8 && s + 1 < nsteps) {   // every wave is past the last tap of round r
+        if (!xs && t == 8 && s + 1 < nsteps) {   // every wave is past the last tap of round r
             if (chunk_of(r + 1) < cend) store_halo();
+            if constexpr (XF) {
+                if (r + 1 == nrounds && nx > 0) store_x(0, stx);   // step NH: the parity opposite to s = NH - 1
+            }
             __syncthreads();
         }
     };
@@ -636,16 +802,21 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     if (nsteps > 0) {
         load_w(0, wx_h, wx_l);
         if (nsteps > 1) load_w(1, wy_h, wy_l);
-        if (chunk_of(0) < cend) {
+        if (NH > 0 && chunk_of(0) < cend) {
             load_halo(chunk_of(0));
             store_w(0, wx_h, wx_l);
             store_halo();
+        } else if (XF && NH == 0 && nx > 0) {   // no halo chunk in this split: X steps only
+            load_x(0, xr0);                 // step 0 (even): set xr0, step 1: xr1
+            if (nx > 1) load_x(1, xr1);
+            store_w(0, wx_h, wx_l);
+            store_x(0, xr0);
         }
         __syncthreads();
         CFD_STAMP(a.stamps, 3, a.seq, 2);
         for (int s = 0; s < nsteps; s += 2) {
-            step(s, wx_h, wx_l, wy_h, wy_l);
-            if (s + 1 < nsteps) step(s + 1, wy_h, wy_l, wx_h, wx_l);
+            step(s, wx_h, wx_l, wy_h, wy_l, xr0, xr1);
+            if (s + 1 < nsteps) step(s + 1, wy_h, wy_l, wx_h, wx_l, xr1, xr0);
         }
     }
 
@@ -697,7 +868,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
 
     const int n_base = n0 + wn * 64 + l32;
     const int p_base = wm * 64 + 4 * hsel;   // tile position of acc element 0 of block 0
-    auto pix_of = [&](int p) { return mrow0 + (int64_t)(p / TW) * W + (p % TW); };
+    auto pix_of = [&](int p) __attribute__((always_inline)) { return mrow0 + (int64_t)(p / TW) * W + (p % TW); };
     if constexpr (KG == 1) {
         // epilogue through LDS (launch_conv's ldsepi: Cout % 4 == 0, 16-B rows): one
         // 64-pixel wave row of the tile at a time is parked in LDS and leaves as
@@ -732,6 +903,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                         f4 v = *(const f4*)(stg + p * BN + c);
                         if (!split) {
                             if (a.bias) v = v + *(const f4*)(a.bias + n);
+                            if (XF && a.bias2) v = v + *(const f4*)(a.bias2 + n);
                             if (a.emb) v = v + *(const f4*)(a.emb + (int64_t)bimg * a.emb_stride + n);
                             if (a.res) v = *(const f4*)(a.res + m * a.Cout + n) + v;
                         }
@@ -776,6 +948,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                 const int n = n_base + 32 * j;
                 if (n >= a.Cout) continue;
                 float v = a.bias ? acc[i][j][e] + a.bias[n] : acc[i][j][e];
+                if (XF && a.bias2) v = v + a.bias2[n];
                 if (a.emb) v = v + a.emb[(int64_t)bimg * a.emb_stride + n];
                 if (a.res) v = a.res[(int64_t)m * a.Cout + n] + v;
                 a.out[(int64_t)m * a.Cout + n] = v;
@@ -810,9 +983,11 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
                         (int64_t)a.Cout * a.K * 2 < (1ll << 31) && a.ks * a.ks <= 9,
                     CFD_ESHAPE, "conv_x: operands beyond 2 GiB");
     }
-    auto grid = [&](int bm, int bn) {
+    auto grid = [&](int bm, int bn) __attribute__((always_inline)) {
         return dim3((unsigned)ceil_div(a.M, bm), (unsigned)ceil_div(a.Cout, bn), splits);
     };
+    CFD_REQUIRE(!a.xsrc1 || variant == 1 || variant == 2 || variant == 20, CFD_ESTATE,
+                "internal: a fused skip convolution runs on K1h / K1x only");
     if (variant == 22) {   // K1hb: bf16 operands, 256-pixel blocks
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0 && !a.wlo, CFD_ESHAPE, "conv_h bf16: 3x3 stride-1 with a 16/32/64-divisible width");
@@ -879,18 +1054,40 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         // (CFD_CONV_SMALLN=0 keeps 128)
         static const int smalln = smalln_below();
         const dim3 g = grid(256, 128);
+        const bool xf = a.xsrc1 != nullptr;   // fused skip convolution (the XF instances)
         if ((int64_t)g.x * g.y * g.z < smalln && a.Cout % 64 == 0) {
             const dim3 g64 = grid(256, 64);
-            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, false, false, 64>), g64, dim3(256), 0, st, a);
-            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, false, false, 64>), g64, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, false, false, 64>), g64, dim3(256), 0, st, a);
+            if (xf) {
+                if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, false, false, 64, 1, true>), g64, dim3(256), 0, st, a);
+                else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, false, false, 64, 1, true>), g64, dim3(256), 0, st, a);
+                else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, false, false, 64, 1, true>), g64, dim3(256), 0, st, a);
+            } else {
+                if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, false, false, 64>), g64, dim3(256), 0, st, a);
+                else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, false, false, 64>), g64, dim3(256), 0, st, a);
+                else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, false, false, 64>), g64, dim3(256), 0, st, a);
+            }
             check_launch("conv_h_kernel");
             return splits;
         }
-        if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
-        else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
+        if (xf) {
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, false, false, 128, 1, true>), g, dim3(512), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32, 1, false, false, 128, 1, true>), g, dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16, 1, false, false, 128, 1, true>), g, dim3(512), 0, st, a);
+        } else {
+            if (tw == 64) hipLaunchKernelGGL((conv_h_kernel<256, 64>), g, dim3(512), 0, st, a);
+            else if (tw == 32) hipLaunchKernelGGL((conv_h_kernel<256, 32>), g, dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
+        }
         check_launch("conv_h_kernel");
+        return splits;
+    }
+    if (a.xsrc1) {   // fused skip convolution
+        switch (variant) {
+            case 1: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1, 1, true>), grid(128, 128), dim3(256), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1, 1, true>), grid(256, 128), dim3(512), 0, st, a); break;
+            default: CFD_REQUIRE(false, CFD_EARG, "conv_x variant");
+        }
+        check_launch("conv_x_kernel");
         return splits;
     }
     switch (variant) {

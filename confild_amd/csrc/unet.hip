@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstring>
 #include <cmath>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -78,12 +79,6 @@ struct cfd_unet {
     int tape_mode = CFD_TAPE_INPUT_VJP;   // what the next forward_tape records
     int tape_mode_rec = CFD_TAPE_INPUT_VJP;   // what the last forward_tape recorded (the replays' layout)
     int* nonfinite = nullptr;  // range guard flag: set by the last convolution on a non-finite eps
-    // side stream of the forward (CFD_UNET_SIDE): the skip 1x1 convolutions and the
-    // timestep-embedding MLP, which depend on nothing the main stream computes next,
-    // run beside it and join before their consumer (event fork / join: captured
-    // into the samplers' HIP graphs as parallel branches)
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     mutable std::map<int, size_t> ws_cache;  // workspace bytes per B (the dry walk is host work)
     uint64_t version = 0;   // bumped by every set_param / set_compute: launch arguments (weight
                             // scales, kernel choice) captured into a graph are stale after it
@@ -414,7 +409,6 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     // normalised (+SiLU) input of the next conv (widest: an output block's concat)
     float* nbuf = ws.take((size_t)B * z.max_cat);
     float* splitk = ws.take(kSplitCap);
-    float* splitk_side = ws.take(kSplitCap);   // the side stream's split-K slab (skip convolutions)
     float* kvws = ws.take((size_t)B * z.max_kvf);
     float* pool[3];
     for (auto& p : pool) p = ws.take((size_t)B * z.max_act);
@@ -441,37 +435,13 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         throw cfd::Error{CFD_ESTATE, "internal: buffer pool exhausted"};
     };
 
-    // the side stream (CFD_UNET_SIDE=0: everything on st).  join_pending: the main
-    // stream must wait for the side stream before the next consumer of its result
-    static const int side_env = getenv("CFD_UNET_SIDE") ? atoi(getenv("CFD_UNET_SIDE")) : 1;
-    const bool use_side = side_env && launch && h->side;
-    bool join_pending = false;
-    auto fork = [&]() {
-        CFD_HIP(hipEventRecord(h->ev_fork, st));
-        CFD_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-    };
-    auto join_mark = [&]() {
-        CFD_HIP(hipEventRecord(h->ev_join, h->side));
-        join_pending = true;
-    };
-    auto join = [&]() {
-        if (!join_pending) return;
-        CFD_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
-        join_pending = false;
-    };
-
-    // timestep embedding + time_embed MLP + every ResBlock's emb_layers (nn.py:118-136,
-    // unet.py:648,199-205): on the side stream, beside conv_in and the first GroupNorm;
-    // joined before the first convolution that adds emb
+    // timestep embedding + time_embed MLP + every ResBlock's emb_layers (nn.py:118-136, unet.py:648,199-205)
     if (launch) {
-        const hipStream_t es = use_side ? h->side : st;
-        if (use_side) fork();
-        cfd::launch_temb(t, h->freqs, temb, mc, B, es);
-        cfd::launch_linear(temb, P(h, "time_embed.0.weight"), P(h, "time_embed.0.bias"), h1, B, mc, h->tdim, 0, es);
+        cfd::launch_temb(t, h->freqs, temb, mc, B, st);
+        cfd::launch_linear(temb, P(h, "time_embed.0.weight"), P(h, "time_embed.0.bias"), h1, B, mc, h->tdim, 0, st);
         cfd::launch_linear(h1, P(h, "time_embed.2.weight"), P(h, "time_embed.2.bias"), emb, B, h->tdim, h->tdim, 1,
-                           es);
-        cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, es);
-        if (use_side) join_mark();
+                           st);
+        cfd::launch_linear(emb, h->emb_w, h->emb_b, embo, B, h->tdim, h->emb_total, 1, st);
     }
 
     // A split-K convolution's reduction is deferred to its consumer: the
@@ -527,10 +497,11 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             g.kpart = pend.a.part;
             g.ksplits = pend.splits;
             g.kbias = pend.a.bias;
+            g.kbias2 = pend.a.bias2;
             g.kemb = pend.a.emb;
             g.kemb_stride = pend.a.emb_stride;
             g.kres = pend.a.res;
-            g.kx = keep_raw ? pend.a.out : nullptr;
+            g.kx = keep_raw || cfd::gn2_applies(g) ? pend.a.out : nullptr;
             pend.splits = 0;
         } else {
             flush();
@@ -586,18 +557,61 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         const cfd::ConvArgs a = conv_args(n, pre, cout, 3, 1, 0, nullptr, nullptr, nullptr);
         return a.wbf && !a.wlo && cfd::conv_runs_k1hb(a, plan_checked(a, kSplitCap));
     };
+    // tweak: adjusts the launch arguments once the plan is known (the qkv K / V pack);
+    // a fused skip convolution (ConvArgs::xsrc1, fuse_skip) is planned as one GEMM
+    using Tweak = std::function<void(cfd::ConvArgs&, const cfd::ConvPlan&)>;
+    // A ResBlock's skip 1x1 convolution (unet.py:255-256) fused into its out_layers
+    // convolution as extra K over the raw block input x: out = [W_out | W_skip] x
+    // [h taps | x] + b_out + b_skip, one GEMM on K1h / K1x, no skip tensor.  The two
+    // weight packs keep their power-of-two scales; the operand of the smaller scale's
+    // side is staged times the ratio (<= 1, exact), acc_scale undoes the other.
+    // Returns false (args untouched) where the plan cannot take it: the skip runs as
+    // its own convolution then.  Off by default (CFD_CONV_SKIPFUSE=1: on, K1h only;
+    // 2: K1x too): measured 3.99 vs 3.97 ms per config-B B = 8 step, 3.07-3.09 vs
+    // 3.04-3.07 at B = 1 (graph loop, same box) -- the X steps, one 32-channel chunk
+    // each behind a two-step prefetch, cost what the separate launch did.
+    static const int skipfuse = getenv("CFD_CONV_SKIPFUSE") ? atoi(getenv("CFD_CONV_SKIPFUSE")) : 0;
+    auto fuse_skip = [&](const Act& hn, const Act& x, const std::string& pre, int cout, float* out,
+                         cfd::ConvArgs* fa) -> bool {
+        if (!skipfuse || h->compute != CFD_COMPUTE_SPLIT_F16) return false;
+        cfd::ConvArgs a = conv_args(hn, pre + ".out_layers.3", cout, 3, 1, 0, nullptr, nullptr, out);
+        float inv_x = 1.f;
+        a.xsrc1 = x.a;
+        a.xsrc2 = x.b;
+        a.XC1 = x.Ca;
+        a.XC2 = x.Cb;
+        a.xwbf = PB(h, pre + ".skip_connection.weight");
+        a.xwlo = PL(h, pre + ".skip_connection.weight", &inv_x);
+        a.bias2 = P(h, pre + ".skip_connection.bias");
+        const float inv_o = a.acc_scale;
+        if (inv_x >= inv_o) {
+            a.main_scale = inv_o / inv_x;
+            a.x_scale = 1.f;
+            a.acc_scale = inv_x;
+        } else {
+            a.main_scale = 1.f;
+            a.x_scale = inv_x / inv_o;
+            a.acc_scale = inv_o;
+        }
+        a.K += x.C();
+        if (!cfd::conv_takes_skip(a, plan_checked(a, kSplitCap))) return false;
+        *fa = a;
+        return true;
+    };
     auto conv = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up,
-                    const float* embp, const float* resp, float* out) {
-        const cfd::ConvArgs a = conv_args(in, pre, cout, ks, stride, up, embp, resp, out);
+                    const float* embp, const float* resp, float* out, const Tweak& tweak = {},
+                    const cfd::ConvArgs* fused = nullptr) {
+        cfd::ConvArgs a = fused ? *fused : conv_args(in, pre, cout, ks, stride, up, embp, resp, out);
         flush();
         const cfd::ConvPlan plan = plan_checked(a, kSplitCap);
+        if (tweak) tweak(a, plan);
         CFD_REQUIRE(!a.src_bf16 || cfd::conv_runs_k1hb(a, plan), CFD_ESTATE,
                     "internal: bf16 GroupNorm output feeds a convolution other than K1hb at " + pre);
         static const int conv_log = getenv("CFD_CONV_LOG") ? atoi(getenv("CFD_CONV_LOG")) : 0;
         if (conv_log && launch)   // development: one line per convolution, in launch order
-            fprintf(stderr, "CONV %s %dx%d C=%d+%d->%d ks=%d s=%d up=%d M=%d kx=%d bm=%d bn=%d nw=%d splits=%d\n",
+            fprintf(stderr, "CONV %s %dx%d C=%d+%d->%d ks=%d s=%d up=%d M=%d kx=%d bm=%d bn=%d nw=%d splits=%d xc=%d\n",
                     pre.c_str(), a.Hin, a.Win, a.C1, a.C2, a.Cout, a.ks, a.stride, a.up, a.M, plan.kx, plan.bm,
-                    plan.bn, plan.nw, plan.splits);
+                    plan.bn, plan.nw, plan.splits, a.XC1 + a.XC2);
         if (launch) {
             const int sp = cfd::launch_conv(a, plan, st, /*defer=*/true);   // the splits it left to reduce
             if (sp > 1) {
@@ -672,42 +686,31 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 // h = in_layers(x) + emb_layers(emb)   (unet.py:236-254)
                 const Act xin = gn(cur, r.pre + ".in_layers.0", 1, &rec.ss1, &rec.st1, true,
                                    feeds_k1hb(cur, r.pre + ".in_layers.2", r.cout), &rec.act1, &rec.amx1);
-                // skip(x) first (its split-K reduction is flushed by the next
-                // convolution), so that in_layers' deferred reduction meets the
-                // out_layers GroupNorm directly   (unet.py:255-256)
-                const float* resp;
-                bool skip_side = false;
-                if (r.cin != r.cout && use_side) {
-                    // on the side stream, beside in_layers and the out_layers GroupNorm:
-                    // it reads only the block input (reduced by the GroupNorm above), its
-                    // own split-K slab, and reduces there (no deferral)
-                    join();          // the previous side work (emb) is consumed first
-                    flush();
-                    fork();
-                    cfd::ConvArgs a = conv_args(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
-                    a.part = splitk_side;
-                    const cfd::ConvPlan plan = plan_checked(a, kSplitCap);
-                    cfd::launch_conv(a, plan, h->side, /*defer=*/false);
-                    join_mark();
-                    skip_side = true;
-                    resp = skipb;
-                } else if (r.cin != r.cout) {
-                    conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
-                    resp = skipb;
+                // skip(x) (unet.py:255-256): fused into the out_layers convolution
+                // below where the plan takes it, else its own convolution just before
+                // it (in_layers' deferred reduction still meets the out_layers GroupNorm)
+                const float* resp = nullptr;
+                if (r.cin != r.cout) {
+                    resp = skipb;   // unless the out_layers convolution takes it (fuse_skip below)
                 } else {
                     CFD_REQUIRE(cur.b == nullptr, CFD_ESTATE, "identity skip on a concatenated input");
                     resp = cur.a;
                 }
                 float* hb = tape ? keep(nout) : tmp;
-                if (!skip_side) join();   // emb (the side stream's first work) before its first consumer
                 conv(xin, r.pre + ".in_layers.2", r.cout, 3, 1, 0, embo + r.emb_off, nullptr, hb);
                 rec.h1 = hb;
                 const Act th{hb, r.cout, nullptr, 0, cur.H, cur.W};
                 const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2, /*keep_raw=*/tape != nullptr,
                                   feeds_k1hb(th, r.pre + ".out_layers.3", r.cout), &rec.act2, &rec.amx2);
                 float* out = dest(cur.a, cur.b, nout);
-                if (skip_side) join();
-                conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
+                cfd::ConvArgs fa{};
+                if (r.cin != r.cout && fuse_skip(hn, cur, r.pre, r.cout, out, &fa)) {
+                    conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, nullptr, out, {}, &fa);
+                } else {
+                    if (r.cin != r.cout)   // reads the block input, still intact: out is another buffer
+                        conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
+                    conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
+                }
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};
                 break;
             }
@@ -717,8 +720,23 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 const Act xn = gn(cur, at.pre + ".norm", 0, &rec.ss1, &rec.st1, true, false, &rec.act1, &rec.amx1);
                 float* qb = tape ? keep((size_t)B * T * 3 * at.C) : qkv;
                 float* ob = tape ? keep((size_t)B * T * at.C) : abuf;
-                conv(xn, at.pre + ".qkv", 3 * at.C, 1, 1, 0, nullptr, nullptr, qb);
-                cfd::AttnArgs aa{qb, ob, T, at.C, (float)(1.0 / std::sqrt(std::sqrt((double)at.ch))), nullptr};
+                const float attn_scale = (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)));
+                const bool split_attn = h->compute != CFD_COMPUTE_F32 && (at.ch == 32 || at.ch == 64 || at.ch == 128);
+                bool kv_packed = false;
+                // the qkv convolution; in split compute its epilogue also packs K / V
+                conv(xn, at.pre + ".qkv", 3 * at.C, 1, 1, 0, nullptr, nullptr, qb,
+                     [&](cfd::ConvArgs& a, const cfd::ConvPlan& plan) {
+                         if (!split_attn || h->compute != CFD_COMPUTE_SPLIT_F16 || !cfd::conv_kv_pack_ok(a, plan, T))
+                             return;
+                         a.kvf = kvws;
+                         a.kv_voff = cfd::attention_split_voff(T, at.ch, at.heads, B);
+                         a.kv_ch = at.ch;
+                         a.kv_heads = at.heads;
+                         a.kv_T = T;
+                         a.kv_scale = attn_scale;
+                         kv_packed = true;
+                     });
+                cfd::AttnArgs aa{qb, ob, T, at.C, attn_scale, nullptr};
                 if (tape) aa.lse = keep((size_t)B * at.heads * T);
                 rec.qkv = qb;
                 rec.o = ob;
@@ -729,8 +747,8 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     // reference's fp16 contract runs q.k and a.v in the low precision with an fp32
                     // softmax (unet.py:349-353), so fp32-level attention is within it; the exact
                     // fp32-MFMA kernel K4 stays for CFD_COMPUTE_F32
-                    if (h->compute != CFD_COMPUTE_F32 && (at.ch == 32 || at.ch == 64 || at.ch == 128))
-                        cfd::launch_attention_split(aa, at.ch, at.heads, B, kvws, st);
+                    if (split_attn)
+                        cfd::launch_attention_split(aa, at.ch, at.heads, B, kvws, st, kv_packed);
                     else
                         cfd::launch_attention(aa, at.ch, at.heads, B, st);
                 }
@@ -776,7 +794,6 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         if (recs) (*recs)[si] = rec;
     }
     flush();
-    join();
 }
 
 
@@ -1185,9 +1202,6 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             CFD_HIP(hipMalloc(&h->freqs, sizeof(float) * std::max(half, 1)));
             CFD_HIP(hipMalloc(&h->nonfinite, sizeof(int)));
             CFD_HIP(hipMemset(h->nonfinite, 0, sizeof(int)));
-            CFD_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-            CFD_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-            CFD_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
             CFD_HIP(hipMemcpy(h->freqs, fr.data(), sizeof(float) * half, hipMemcpyHostToDevice));
         } catch (...) {
             cfd_unet_destroy(h);
@@ -1215,9 +1229,6 @@ extern "C" void cfd_unet_destroy(cfd_unet* h) {
     (void)hipFree(h->rp_part);
     (void)hipFree(h->rp_amax);
     (void)hipFree(h->rp_tfirst);
-    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
-    if (h->side) (void)hipStreamDestroy(h->side);
     delete h;
 }
 

@@ -317,10 +317,11 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     if (ksrc) {  // constant false for IPT > 16: the branch folds away
         // split-K source (GnArgs::kpart): reduce, epilogue, store x, keep it
         const int64_t slab = (int64_t)a.B * HW * a.C1;
-        f4 kb = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
+        f4 kb = {0.f, 0.f, 0.f, 0.f}, kb2 = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (a.kbias) kb[j] = a.kbias[c + j];
+            if (a.kbias2) kb2[j] = a.kbias2[c + j];
             if (a.kemb) ke[j] = a.kemb[b * a.kemb_stride + c + j];
         }
         // every load first (the partials, then the residual), every store after:
@@ -370,6 +371,7 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float y = a.kbias ? v[k][j] + kb[j] : v[k][j];
+                    if (a.kbias2) y = y + kb2[j];   // a fused skip convolution's bias
                     if (a.kemb) y = y + ke[j];
                     if (kres) y = rs[k][j] + y;
                     v[k][j] = y;
@@ -463,6 +465,212 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// K3c: GroupNorm(32)(+SiLU) in two launches over pixel chunks, full pixel rows
+// (every channel of a pixel: 512-B lines read once, not one 16-B group slice per
+// workgroup and line).  gn2_stats: per (chunk, sample) the per-group float64 sum
+// and sum of squares of its pixels (a split-K source reduced on the way, as the
+// register kernel does, and its sum stored at kx); gn2_apply: every workgroup
+// reduces its sample's chunk partials itself (fixed order, identical on every
+// workgroup), forms scale / shift and normalises its chunk.  The chunk count is a
+// function of HW only, so a sample's statistics do not depend on the batch.  For
+// the large latents (config E 128^2) and, with more workgroups than groups, the
+// small batches.
+// ---------------------------------------------------------------------------
+int gn2_chunks(int HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 16)); }
+
+__global__ __launch_bounds__(256) void gn2_stats_kernel(GnArgs a) {
+    const int chunk = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    const int Ctot = a.Ctot, cq = Ctot / 4, cpg = Ctot / 32;
+    const int HW = a.HW, NC = gridDim.x;
+    const int p0 = (int)((int64_t)HW * chunk / NC), p1 = (int)((int64_t)HW * (chunk + 1) / NC);
+    const int rows = 256 / cq;
+    const int q = threadIdx.x % cq, r0 = threadIdx.x / cq;
+    const int c0 = 4 * q;
+    const bool act = r0 < rows;
+    const bool ksrc = a.kpart && c0 < a.C1;
+    __shared__ double red[2][1024];
+    double s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+    f4 kb = {0.f, 0.f, 0.f, 0.f}, kb2 = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
+    if (ksrc) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (a.kbias) kb[j] = a.kbias[c0 + j];
+            if (a.kbias2) kb2[j] = a.kbias2[c0 + j];
+            if (a.kemb) ke[j] = a.kemb[b * a.kemb_stride + c0 + j];
+        }
+    }
+    const int64_t slab = (int64_t)a.B * HW * a.C1;
+    constexpr int U = 4;   // pixel rows in flight per thread
+    if (act) {
+        for (int pb = p0 + r0; pb < p1; pb += U * rows) {
+            f4 v[U];
+            if (ksrc) {   // splitk_reduce's order: slab 0, the others in split order, bias, emb, residual
+                f4 rs[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int p = pb + u * rows;
+                    const int64_t e = (b * HW + p) * a.C1 + c0;
+                    rs[u] = a.kres && p < p1 ? *(const f4*)(a.kres + e) : f4{0.f, 0.f, 0.f, 0.f};
+                    v[u] = p < p1 ? *(const f4*)(a.kpart + e) : f4{0.f, 0.f, 0.f, 0.f};
+                }
+                for (int sp = 1; sp < a.ksplits; ++sp) {
+                    f4 w[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int p = pb + u * rows;
+                        w[u] = p < p1 ? *(const f4*)(a.kpart + sp * slab + (b * HW + p) * a.C1 + c0)
+                                      : f4{0.f, 0.f, 0.f, 0.f};
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) v[u] += w[u];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int p = pb + u * rows;
+                    if (p >= p1) continue;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float y = a.kbias ? v[u][j] + kb[j] : v[u][j];
+                        if (a.kbias2) y = y + kb2[j];
+                        if (a.kemb) y = y + ke[j];
+                        if (a.kres) y = rs[u][j] + y;
+                        v[u][j] = y;
+                    }
+                    *(f4*)(a.kx + (b * HW + p) * a.C1 + c0) = v[u];
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int p = pb + u * rows;
+                    const int64_t pix = b * HW + p;
+                    v[u] = p >= p1 ? f4{0.f, 0.f, 0.f, 0.f}
+                         : c0 < a.C1 ? *(const f4*)(a.src1 + pix * a.C1 + c0)
+                                     : *(const f4*)(a.src2 + pix * a.C2 + (c0 - a.C1));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {   // zero padding adds nothing
+                    s[j] += v[u][j];
+                    s2[j] += (double)v[u][j] * v[u][j];
+                }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            red[0][r0 * Ctot + c0 + j] = s[j];
+            red[1][r0 * Ctot + c0 + j] = s2[j];
+        }
+    }
+    __syncthreads();
+    // per group: its channels over the rows, fixed order (8 lanes per group, then a
+    // fixed-order combine of the 8)
+    const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
+    double ts = 0, ts2 = 0;
+    for (int e = sub; e < rows * cpg; e += 8) {
+        const int r = e / cpg, c = grp * cpg + (e - r * cpg);
+        ts += red[0][r * Ctot + c];
+        ts2 += red[1][r * Ctot + c];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {   // xor butterfly: the same sum on all 8 lanes
+        ts += __shfl_xor(ts, o);
+        ts2 += __shfl_xor(ts2, o);
+    }
+    if (sub == 0) {
+        double* dst = a.part + ((b * NC + chunk) * 32 + grp) * 2;
+        dst[0] = ts;
+        dst[1] = ts2;
+    }
+}
+
+__global__ __launch_bounds__(256) void gn2_apply_kernel(GnArgs a) {
+    const int chunk = blockIdx.x;
+    const int64_t b = blockIdx.y;
+    const int Ctot = a.Ctot, cq = Ctot / 4, cpg = Ctot / 32;
+    const int HW = a.HW, NC = gridDim.x;
+    __shared__ float ssh[2][1024];
+    {   // the sample's statistics from the chunk partials: 8 lanes per group, every
+        // 8th chunk in chunk order, then an xor butterfly (the same value on every lane)
+        const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
+        double S = 0, S2 = 0;
+        for (int k = sub; k < NC; k += 8) {
+            const double2 v = *(const double2*)(a.part + ((b * NC + k) * 32 + grp) * 2);
+            S += v.x;
+            S2 += v.y;
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            S += __shfl_xor(S, o);
+            S2 += __shfl_xor(S2, o);
+        }
+        const double n = (double)HW * cpg;
+        const double mean = S / n;
+        const double var = fmax(S2 / n - mean * mean, 0.0);
+        const float mf = (float)mean, rf = (float)(1.0 / sqrt(var + (double)a.eps));
+        if (sub < cpg) {   // this group's channels (cpg <= 32: 8 lanes, a few each)
+            for (int cc = sub; cc < cpg; cc += 8) {
+                const int c = grp * cpg + cc;
+                const float sc = rf * a.gamma[c];
+                const float sf = a.beta[c] - mf * sc;
+                ssh[0][c] = sc;
+                ssh[1][c] = sf;
+                if (chunk == 0) {
+                    a.ss[(b * Ctot + c) * 2 + 0] = sc;
+                    a.ss[(b * Ctot + c) * 2 + 1] = sf;
+                }
+            }
+        }
+        if (a.stats && chunk == 0 && sub == 0) {
+            a.stats[(b * 32 + grp) * 2 + 0] = mf;
+            a.stats[(b * 32 + grp) * 2 + 1] = rf;
+        }
+    }
+    __syncthreads();
+    const int p0 = (int)((int64_t)HW * chunk / NC), p1 = (int)((int64_t)HW * (chunk + 1) / NC);
+    const int rows = 256 / cq;
+    const int q = threadIdx.x % cq, r0 = threadIdx.x / cq;
+    const int c0 = 4 * q;
+    float mx = 0.f;
+    if (r0 < rows) {
+        f4 sc, sf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sc[j] = ssh[0][c0 + j];
+            sf[j] = ssh[1][c0 + j];
+        }
+        // the raw input: a split-K source was reduced into kx by gn2_stats
+        const bool kin = a.kpart && c0 < a.C1;
+        const float* xs = kin ? a.kx : c0 < a.C1 ? a.src1 : a.src2;
+        const int ld = c0 < a.C1 ? a.C1 : a.C2, cx = c0 < a.C1 ? c0 : c0 - a.C1;
+        constexpr int U = 4;
+        for (int pb = p0 + r0; pb < p1; pb += U * rows) {
+            f4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int p = pb + u * rows;
+                v[u] = p < p1 ? *(const f4*)(xs + (b * HW + p) * ld + cx) : f4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int p = pb + u * rows;
+                if (p >= p1) continue;
+                f4 y;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    y[j] = v[u][j] * sc[j] + sf[j];
+                    if (a.silu) y[j] = silu_f(y[j]);
+                }
+                gn_store4(a, (b * HW + p) * Ctot + c0, y);
+                mx = fmaxf(mx, amax4(y));
+            }
+        }
+    }
+    if (a.amax_out) block_amax_atomic(mx, a.amax_out);
+}
+
+// ---------------------------------------------------------------------------
 // K1/K2: implicit-GEMM convolution.  GEMM view: M = B*Hout*Wout output pixels,
 // N = Cout, K = ks*ks*Ctot ordered (tap, channel).  Workgroup tile BM x BN x 32,
 // 4 waves as 2x2, each wave (BM/2)x(BN/2) of 16x16 fp32 MFMA tiles.
@@ -505,6 +713,20 @@ __device__ __forceinline__ void split4_mix(const f4& x, uint2& hi, uint2& lo) {
     asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.x) : "v"(x[1]), "v"(hi.x));
     asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo.y) : "v"(x[2]), "v"(hi.y));
     asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.y) : "v"(x[3]), "v"(hi.y));
+}
+
+// the K scale of the split attention: q.k scale times log2 e (S in base-2 units)
+__device__ __forceinline__ float kln2(float scale) { return scale * 1.44269504088896340736f; }
+// hi / lo f16 halves of 8 fp32 values (the split attention's fragment operands)
+// (contraction off: v - hi must not fuse with a multiply that formed v in the
+// caller, so the qkv epilogue's K pack and attn_kv_split round identically)
+__device__ __forceinline__ void split8_f16(const float (&v)[8], h8v& hi, h8v& lo) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        hi[t] = (_Float16)v[t];
+        lo[t] = (_Float16)(v[t] - (float)hi[t]);
+    }
 }
 
 // SPLIT (MODE 2, default fp32 path): fp32-accurate convolution on f16 MFMA.
@@ -931,6 +1153,65 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                 *(f4*)(a.out + o) = val;
             }
           }
+          // qkv convolution: the split attention's K / V fragments from the staged
+          // tile (still whole in LDS: one band), attn_kv_split_kernel's layout and
+          // arithmetic -- K = (acc + bias) * scale log2 e, V = acc + bias, each split
+          // into f16 hi / lo -- so the same bits, without its launch and its re-read
+          // of qkv.  T % 32 == 0 (conv_kv_pack_ok): a 32-key block never straddles
+          // two samples and T32 = T.
+          if constexpr (SP && EPI_PASSES == 1) {
+            if (a.kvf && gridDim.z == 1) {
+              const float* tile = smem_ab;
+              auto sw = [](int row, int col) { return row * BN + (col ^ (((row >> 2) & 3) << 4)); };
+              const int CH = a.kv_ch, C3 = 3 * CH, T = a.kv_T, nj = CH >> 5, nd = CH >> 4;
+              const float ks = kln2(a.kv_scale);
+              h8v* kf = (h8v*)a.kvf;
+              h8v* vf = kf + a.kv_voff;
+              // K: (key row, 8 channels) -> one lane of fragment (key / 16, j)
+              for (int it = tid; it < BM * (BN / 8); it += 64 * NW) {
+                  const int row = it / (BN / 8), c8 = (it - row * (BN / 8)) * 8;
+                  const int m = m0 + row, n = n0 + c8;
+                  if (m >= a.M || n >= a.Cout) continue;
+                  const int hh = n / C3, o = n - hh * C3;
+                  if (o < CH || o >= 2 * CH) continue;
+                  const int kc = o - CH, b = m / T, key = m - b * T;
+                  f4 v0 = *(const f4*)&tile[sw(row, c8)], v1 = *(const f4*)&tile[sw(row, c8 + 4)];
+                  v0 = v0 + *(const f4*)(a.bias + n);
+                  v1 = v1 + *(const f4*)(a.bias + n + 4);
+                  float v[8];
+#pragma unroll
+                  for (int t = 0; t < 4; ++t) {
+                      v[t] = v0[t] * ks;
+                      v[t + 4] = v1[t] * ks;
+                  }
+                  h8v hi, lo;
+                  split8_f16(v, hi, lo);
+                  const int64_t bh = (int64_t)b * a.kv_heads + hh;
+                  h8v* dst = kf + ((bh * (T >> 4) + (key >> 4)) * nj + (kc >> 5)) * 128 + ((kc & 31) >> 3) * 16 + (key & 15);
+                  dst[0] = hi;
+                  dst[64] = lo;
+              }
+              // V: (32-key block, lane group g, channel) -> one lane of fragment (block, channel / 16)
+              for (int it = tid; it < (BM / 32) * 4 * BN; it += 64 * NW) {
+                  const int col = it % BN, r2 = it / BN, g = r2 & 3, blk = r2 >> 2;
+                  const int n = n0 + col, mb = m0 + 32 * blk;
+                  if (n >= a.Cout || mb >= a.M) continue;
+                  const int hh = n / C3, o = n - hh * C3;
+                  if (o < 2 * CH) continue;
+                  const int vc = o - 2 * CH, b = mb / T, kb = (mb - b * T) >> 5;
+                  const float bn = a.bias[n];
+                  float v[8];
+#pragma unroll
+                  for (int t = 0; t < 8; ++t) v[t] = tile[sw(32 * blk + (t < 4 ? 4 * g + t : 12 + 4 * g + t), col)] + bn;
+                  h8v hi, lo;
+                  split8_f16(v, hi, lo);
+                  const int64_t bh = (int64_t)b * a.kv_heads + hh;
+                  h8v* dst = vf + ((bh * (T >> 5) + kb) * nd + (vc >> 4)) * 128 + g * 16 + (vc & 15);
+                  dst[0] = hi;
+                  dst[64] = lo;
+              }
+            }
+          }
 #ifdef CFD_STAMPS
             __builtin_amdgcn_s_waitcnt(0);
 #endif
@@ -1005,6 +1286,7 @@ __global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         float y = a.bias ? s[j] + a.bias[n + j] : s[j];
+        if (a.bias2) y = y + a.bias2[n + j];   // a fused skip convolution's bias
         if (a.emb) y = y + a.emb[(int64_t)bb * a.emb_stride + n + j];
         if (a.res) y = rv[j] + y;
         v[j] = y;
@@ -1072,9 +1354,13 @@ __global__ __launch_bounds__(256) void conv_out_vec_kernel(ConvArgs a, int LP) {
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int ppw = 64 / LP;
-    const int64_t m = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * ppw + lane / LP;
     const int c = 4 * (lane % LP);
     const int HW = a.Hout * a.Wout;
+    // grid-stride over pixel groups (launch_conv_out bounds the grid): the weight
+    // table each workgroup stages in LDS serves many pixels, not one wave's ppw
+    for (int64_t m0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * ppw; m0 < a.M;
+         m0 += (int64_t)gridDim.x * (blockDim.x >> 6) * ppw) {
+    const int64_t m = m0 + lane / LP;
     const int64_t mm = m < a.M ? m : a.M - 1;
     const int b = (int)(mm / HW), rem = (int)(mm - (int64_t)b * HW), oy = rem / a.Wout, ox = rem - oy * a.Wout;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1104,6 +1390,7 @@ __global__ __launch_bounds__(256) void conv_out_vec_kernel(ConvArgs a, int LP) {
             if (a.nonfinite && !isfinite(y)) *a.nonfinite = 1;
         }
     }
+    }
 }
 
 // Forward first convolution, C1 <= 4 -> Cout: one thread per (pixel, 4 output
@@ -1117,8 +1404,10 @@ __global__ __launch_bounds__(256) void conv_in_vec_kernel(ConvArgs a) {
     }
     __syncthreads();
     const int nq = Cout / 4;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)a.M * nq) return;
+    // grid-stride (launch_conv_in bounds the grid): the staged weight table serves
+    // many pixels per workgroup instead of 256 / nq
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < (int64_t)a.M * nq;
+         idx += (int64_t)gridDim.x * blockDim.x) {
     const int n0 = 4 * (int)(idx % nq);
     const int64_t m = idx / nq;
     const int HW = a.Hout * a.Wout;
@@ -1141,6 +1430,7 @@ __global__ __launch_bounds__(256) void conv_in_vec_kernel(ConvArgs a) {
         for (int j = 0; j < 4; ++j) s[j] += a.bias[n0 + j];
     }
     *(f4*)(a.out + m * Cout + n0) = s;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1259,16 +1549,8 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 // v_exp_f32 (ocml's expf is ~11 instructions: the softmax was ~1/3 of the loop's
 // issue) and the saved log-sum-exp is converted back to natural units.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float kln2(float scale) { return scale * 1.44269504088896340736f; }
 // s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
 constexpr int vmcnt_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
-__device__ __forceinline__ void split8_f16(const float (&v)[8], h8v& hi, h8v& lo) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        hi[t] = (_Float16)v[t];
-        lo[t] = (_Float16)(v[t] - (float)hi[t]);
-    }
-}
 
 __global__ __launch_bounds__(256) void attn_kv_split_kernel(AttnArgs a, int CH, int heads, int B, h8v* kf,
                                                             h8v* vf) {
@@ -1699,8 +1981,17 @@ static int env_int(const char* name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 
+// the two-launch full-row GroupNorm (gn2_*) for this shape (a function of the
+// per-sample shape only: batch invariance).  CFD_GN2_HW: from this many pixels
+// per sample up (0: never)
+bool gn2_applies(const GnArgs& a) {
+    static const int hw = env_int("CFD_GN2_HW", 0);
+    return hw > 0 && a.HW >= hw && a.Ctot % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0 && a.Ctot <= 1024;
+}
+
 bool gn_takes_splitk(const GnArgs& a, int B) {
     (void)B;
+    if (gn2_applies(a)) return a.C1 % 4 == 0;
     static const int fused = env_int("CFD_GN_FUSED", 1);
     static const int ksrc = env_int("CFD_GN_SPLITK", 1);
     if (!ksrc || fused != 1 || a.Ctot % 128 != 0 || a.C1 % 4 != 0) return false;
@@ -1717,6 +2008,15 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     a.stamps = g_stamps;
     a.seq = g_seq++;
     CFD_REQUIRE(!a.kpart || gn_takes_splitk(a, B), CFD_ESTATE, "internal: split-K source on a GroupNorm path without it");
+    if (gn2_applies(a)) {
+        CFD_REQUIRE(!a.kpart || a.kx, CFD_ESTATE, "internal: gn2 needs the split-K sum's destination");
+        a.nchunks = gn2_chunks(a.HW);
+        hipLaunchKernelGGL(gn2_stats_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
+        check_launch("gn2_stats_kernel");
+        hipLaunchKernelGGL(gn2_apply_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
+        check_launch("gn2_apply_kernel");
+        return;
+    }
     static const int fused = env_int("CFD_GN_FUSED", 1);
     static const int big = env_int("CFD_GN_BIG", 1);   // 0: the one-launch kernels at every size
     static const int nt1024 = env_int("CFD_GN_NT1024", 1);
@@ -1933,6 +2233,29 @@ static bool conv_x_falls_back(const ConvArgs& a) {
 
 bool conv_runs_k1hb(const ConvArgs& a, const ConvPlan& p) { return p.kx == 22 && !conv_x_falls_back(a); }
 
+bool conv_takes_skip(const ConvArgs& a, const ConvPlan& p) {
+    static const int khg = env_int("CFD_CONV_KHG", 0);
+    const int XC = a.XC1 + a.XC2;
+    const bool kgroups = p.kx == 20 && p.splits == 2 && khg > 0 && a.Cout % 64 == 0 &&
+                         ceil_div(a.M, 256) * ceil_div(a.Cout, 64) >= khg;   // launch_conv's variant 24
+    // K1h only: the K1x form (conv_x_kernel<..., XF>) is built but keeps part of its
+    // arguments in scratch (measured first: CFD_CONV_SKIPFUSE=2 also takes it)
+    static const int kx_too = env_int("CFD_CONV_SKIPFUSE", 0) == 2;
+    return (p.kx == 20 || (kx_too && (p.kx == 1 || p.kx == 2))) && !kgroups && !conv_x_falls_back(a) && a.wbf && a.wlo &&
+           a.xwbf && a.xwlo && !a.tmode && !a.up && a.ks == 3 && a.stride == 1 && !a.src_bf16 && XC > 0 &&
+           XC % 32 == 0 && a.XC1 % 4 == 0 && a.XC2 % 4 == 0 && (int64_t)a.M * std::max(a.XC1, a.XC2) * 4 < (1ll << 31) &&
+           (int64_t)a.Cout * XC * 2 < (1ll << 31) && (p.kx != 20 || conv_h_tw(a) > 0);
+}
+
+bool conv_kv_pack_ok(const ConvArgs& a, const ConvPlan& p, int T) {
+    // launch_conv's choices: K1s (a 1x1 never takes K1x unless CFD_CONV_KX1), split
+    // compute (MODE 2: a one-band LDS epilogue), the LDS epilogue on, one split
+    static const int ldsepi = env_int("CFD_CONV_LDSEPI", 1);
+    static const int fuse = env_int("CFD_ATTN_KVFUSE", 1);   // 0: the attn_kv_split launch (A/B)
+    return fuse && ldsepi && p.kx < 0 && p.splits == 1 && a.wbf && a.wlo && !a.tmode && a.ks == 1 && a.bias &&
+           !a.emb && !a.res && a.Cout % 8 == 0 && a.emb_stride % 4 == 0 && T % 32 == 0 && a.M % T == 0;
+}
+
 int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defer) {
     ConvPlan p = p0;
     if (p.kx >= 0 && conv_x_falls_back(a)) {
@@ -1946,12 +2269,13 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     static const int pf = env_int("CFD_CONV_PF", 1);
     if (p.kx < 0) p.pf = pf >= 1 && pf <= 3 ? pf : 1;
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
-    CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot, CFD_ESHAPE, "conv K mismatch");
+    CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot + a.XC1 + a.XC2, CFD_ESHAPE, "conv K mismatch");
+    CFD_REQUIRE(!a.xsrc1 || conv_takes_skip(a, p0), CFD_ESTATE, "internal: fused skip convolution on an ineligible plan");
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
     CFD_REQUIRE(!a.tmode || ((a.stride == 1 || a.stride == 2) && !a.up), CFD_ESHAPE, "transposed conv: stride 1|2");
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
     CFD_REQUIRE(!(a.tmode && a.wbf && !a.wlo), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
-    static const int xcd = env_int("CFD_CONV_XCD", 1);
+    static const int xcd = env_int("CFD_CONV_XCD", 3);   // round 5: 3 (PMC: 16^2 K1h L2 hit 0.19-0.27 -> 0.69-0.79)
     static const int korder = env_int("CFD_CONV_KORDER", 0);
     static const int bufaddr = env_int("CFD_CONV_BUFADDR", 1);
     static const int ldsepi = env_int("CFD_CONV_LDSEPI", 1);
@@ -2004,7 +2328,7 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
 void launch_conv_in(const ConvArgs& a, hipStream_t st) {
     if (a.Cout % 4 == 0 && a.C1 <= 4 && (size_t)9 * a.C1 * a.Cout * 4 <= 64 * 1024) {
         const int64_t n = (int64_t)a.M * (a.Cout / 4);
-        hipLaunchKernelGGL(conv_in_vec_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256),
+        hipLaunchKernelGGL(conv_in_vec_kernel, dim3((unsigned)std::min<int64_t>(2048, ceil_div(n, 256))), dim3(256),
                            sizeof(float) * 9 * a.C1 * a.Cout, st, a);
         check_launch("conv_in_vec_kernel");
         return;
@@ -2020,7 +2344,7 @@ void launch_conv_out(const ConvArgs& a, hipStream_t st) {
     if (a.Ctot % 4 == 0 && a.C1 == a.Ctot && LP >= 1 && LP <= 64 && (LP & (LP - 1)) == 0 &&
         (size_t)a.Cout * a.K * 4 <= 64 * 1024) {
         const int64_t waves = ceil_div(a.M, 64 / LP);
-        hipLaunchKernelGGL(conv_out_vec_kernel, dim3((unsigned)ceil_div(waves, 4)), dim3(256),
+        hipLaunchKernelGGL(conv_out_vec_kernel, dim3((unsigned)std::min<int64_t>(2048, ceil_div(waves, 4))), dim3(256),
                            sizeof(float) * a.Cout * a.K, st, a, LP);
         check_launch("conv_out_vec_kernel");
         return;
@@ -2043,15 +2367,22 @@ void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t s
 
 size_t attention_split_floats(int T, int C) { return (size_t)(T + 31) / 32 * 32 * C * 2; }
 
-void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st) {
+int64_t attention_split_voff(int T, int CH, int heads, int B) {
+    const int T32 = (T + 31) / 32 * 32;
+    return (int64_t)B * heads * (T32 / 16) * (CH / 32) * 128;
+}
+
+void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st, bool packed) {
     CFD_REQUIRE(CH == 32 || CH == 64 || CH == 128, CFD_ESHAPE, "split attention needs head channels 32, 64 or 128");
     const int T32 = (a.T + 31) / 32 * 32;
     h8v* kf = (h8v*)kvws;
-    h8v* vf = kf + (size_t)B * heads * (T32 / 16) * (CH / 32) * 128;
-    const int64_t slots = (int64_t)B * heads * ((T32 / 16) * (CH / 32) * 64 + (T32 / 32) * (CH / 16) * 64);
-    hipLaunchKernelGGL(attn_kv_split_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, st, a, CH, heads, B,
-                       kf, vf);
-    check_launch("attn_kv_split_kernel");
+    h8v* vf = kf + attention_split_voff(a.T, CH, heads, B);
+    if (!packed) {   // else the qkv convolution's epilogue wrote them (ConvArgs::kvf)
+        const int64_t slots = (int64_t)B * heads * ((T32 / 16) * (CH / 32) * 64 + (T32 / 32) * (CH / 16) * 64);
+        hipLaunchKernelGGL(attn_kv_split_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, st, a, CH, heads,
+                           B, kf, vf);
+        check_launch("attn_kv_split_kernel");
+    }
     // K4d (default; CFD_ATTN_DMA=0 restores K4s): fragments staged per workgroup
     // by LDS-DMA, 8 waves (128 queries) per workgroup where T >= 512 and that still
     // gives >= 256 workgroups, else 4 -- at batch 1 the 64-query workgroups double

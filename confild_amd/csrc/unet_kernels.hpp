@@ -27,6 +27,7 @@ struct GnArgs {
     const float* kbias;
     const float* kemb;
     const float* kres;
+    const float* kbias2;  // a fused skip convolution's bias (ConvArgs::bias2), or null
     float* kx;           // where the reduced sum is stored (null: nowhere, nobody reads it)
     int ksplits, kemb_stride;
     unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
@@ -66,6 +67,26 @@ struct ConvArgs {
     int ldsepi;          // K1s: epilogue through LDS, float4 rows (set by launch_conv; CFD_CONV_LDSEPI=0: off)
     int* nonfinite;      // conv_out only: set to 1 when an output is not finite (range guard), or null
     int src_bf16;        // src1 / src2 hold bf16 (a GroupNorm's out_bf16 output): K1hb only
+    // qkv convolution on K1s in split compute (conv_kv_pack_ok): the LDS epilogue also
+    // writes the split attention's packed K / V fragments (attn_kv_split_kernel's
+    // layout and arithmetic) from the staged tile, so no pack launch follows
+    void* kvf;           // K fragments (h8v), V fragments at kvf + kv_voff h8v; null: no pack
+    int64_t kv_voff;
+    int kv_ch, kv_heads, kv_T;
+    float kv_scale;      // the attention's q / k scale (K carries scale * log2 e)
+    // fused 1x1 skip convolution (a ResBlock's out_layers in split compute, on K1h /
+    // K1x: conv_takes_skip): XC1 + XC2 more K channels of the raw block input (two
+    // sources, read at the output pixel), weights xwbf / xwlo (Cout, XC1 + XC2) f16
+    // hi / lo, its bias in bias2.  The two weight packs carry their own power-of-two
+    // scales; main_scale / x_scale (powers of two <= 1, exact) scale the operands as
+    // they are staged so both parts accumulate at the scale acc_scale undoes
+    const float* xsrc1;
+    const float* xsrc2;
+    int XC1, XC2;
+    const void* xwbf;
+    const void* xwlo;
+    const float* bias2;
+    float main_scale, x_scale;
     unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
     int seq;                      // launch sequence number (timestamps)
 };
@@ -135,6 +156,9 @@ void launch_gn(const GnArgs& a, int B, hipStream_t st);
 // whether launch_gn runs the register-resident kernel for this shape (the only
 // one that accepts a split-K source, GnArgs::kpart)
 bool gn_takes_splitk(const GnArgs& a, int B);
+// whether launch_gn runs the two-launch full-row form (gn2_*) for this shape: it
+// then needs GnArgs::kx for a split-K source (the apply pass re-reads the sum)
+bool gn2_applies(const GnArgs& a);
 // part_cap_floats: split-K slab available per 8 samples (plans depend on the
 // per-sample shape only, never on the batch)
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats);
@@ -180,7 +204,18 @@ void launch_conv_out(const ConvArgs& a, hipStream_t st);
 void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t st);
 // split-f16 attention (K4s); kvws holds attention_split_floats(T, C) floats per sample
 size_t attention_split_floats(int T, int C);
-void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st);
+// packed: the qkv convolution already wrote the K / V fragments (ConvArgs::kvf)
+void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st,
+                            bool packed = false);
+// the K / V fragment pointers of kvws (launch_attention_split's layout): K at
+// kvws, V at kvws + voff h8v
+int64_t attention_split_voff(int T, int CH, int heads, int B);
+// whether launch_conv runs this qkv plan through a K1s LDS epilogue that can pack
+// the K / V fragments (split compute, no split-K, T % 32 == 0)
+bool conv_kv_pack_ok(const ConvArgs& a, const ConvPlan& p, int T);
+// whether this 3x3 plan can take a fused 1x1 skip convolution (ConvArgs::xsrc1):
+// K1h (256-pixel halo tiles) or K1x in split compute, no fallback to K1s
+bool conv_takes_skip(const ConvArgs& a, const ConvPlan& p);
 // backward (unet_vjp.hip)
 int launch_gn_bwd(const GnbArgs& a, int B, hipStream_t st);   // returns the pixel chunks used
 void launch_attention_bwd(const AttnBwdArgs& a, int CH, int heads, int B, hipStream_t st);

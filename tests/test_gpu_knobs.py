@@ -62,8 +62,43 @@ def _run(env_extra):
 @pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0", "CFD_CONV_KHG=1",
                                   "CFD_CONV_KHB_OCC=0", "CFD_CONV_LDSEPI=0", "CFD_ATTN_XCD=0"])
 def test_schedule_switch_is_bit_identical(hip, knob):
-    base = _run({})
+    # K1h's in-workgroup K groups take no fused skip convolution (conv_takes_skip):
+    # that switch is compared with the skip convolutions unfused on both sides
+    extra = {"CFD_CONV_SKIPFUSE": "0"} if knob.startswith("CFD_CONV_KHG") else {}
+    base = _run(extra)
     k, v = knob.split("=")
-    got = _run({k: v})
+    got = _run(dict(extra, **{k: v}))
     for key in base:
         assert got[key] == base[key], f"{knob} changed eps at {key}"
+
+
+FUSED = r"""
+import ast, json, sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from confild_amd import synth
+from confild_amd.script_util import create_model
+out = {}
+for name in ("small32", "cfgA32", "cfgB64"):
+    g = np.load(f"{sys.argv[1]}/tests/golden/unet_{name}.npz", allow_pickle=False)
+    kw = ast.literal_eval(str(g["kwargs"]))
+    m = create_model(**kw)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in
+                       synth.unet_state_dict(int(g["seed"]), {k: tuple(v.shape) for k, v in m.state_dict().items()}).items()})
+    m.to("cuda")
+    eps = m(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["t"]).cuda()).cpu().numpy()
+    out[name] = float(np.abs(eps - g["eps"]).max() / np.abs(g["eps"]).max())
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_fused_skip_convolution_vs_reference(hip, mode):
+    """The ResBlock skip 1x1 convolution fused into out_layers (CFD_CONV_SKIPFUSE:
+    1 on K1h, 2 on K1x too; off by default, measured slower): the U-Nets with
+    concatenated skips against the reference goldens at the forward's 1e-5."""
+    env = dict(os.environ, CFD_CONV_SKIPFUSE=mode)
+    r = subprocess.run([sys.executable, "-c", FUSED, ROOT], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    errs = json.loads(r.stdout.strip().splitlines()[-1])
+    print(f"fused skip ({mode}) vs reference: {errs}")
+    assert max(errs.values()) <= 1e-5, errs
