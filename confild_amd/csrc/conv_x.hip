@@ -465,7 +465,11 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     };
     constexpr int HPLANE = NPX * 64;                  // one f16 plane of the halo (64 B per pixel)
     constexpr int HIT = (NPX * 8 + NTG - 1) / NTG;    // 16-B halo pieces per thread
-    constexpr int BPLANE = BN * 64, BSTAGE = PL * BPLANE;
+    // TG taps per step: the bf16 form (one MFMA per product) takes a kernel row of 3
+    // taps per step and ring slot, so each barrier is amortised over as many MFMAs as
+    // a split-f16 step's (3 per product, one tap); the split form keeps one tap
+    constexpr int TG = BF ? 3 : 1, SPR = 9 / TG;   // taps per step, steps per chunk
+    constexpr int BPLANE = BN * 64, BSTAGE = PL * BPLANE * TG;
     constexpr int BIT = BN * 4 / NTG;                 // 16-B weight pieces per thread and plane
     constexpr int GBYTES = PL * HPLANE + 2 * BSTAGE;  // one group's halo + weight ring
     static_assert(BM % TW == 0 && BIT >= 1, "tile");
@@ -575,7 +579,8 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
 
     typedef typename std::conditional<SB, uint2, f4>::type HT;   // one halo piece in registers
     HT rh[HIT];
-    u4 wx_h[BIT], wx_l[BIT], wy_h[BIT], wy_l[BIT];   // weight slices two steps deep
+    constexpr int BW = BIT * TG;   // 16-B weight pieces per thread, plane and step
+    u4 wx_h[BW], wx_l[BW], wy_h[BW], wy_l[BW];   // weight slices two steps deep
     auto load_halo = [&](int c) __attribute__((always_inline)) {
         const int cb = 32 * c;
         const bool second = cb >= a.C1;
@@ -624,7 +629,7 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
             }
         }
     };
-    const int NH = nrounds * 9;   // halo steps; the X steps follow
+    const int NH = nrounds * SPR;   // halo steps; the X steps follow
     // X chunk j of this workgroup into a register set / from it into X buffer j & 1.
     // Chunk j lives in the set of its step's parity ((NH + j) & 1: xr0 even, xr1 odd),
     // picked by a uniform branch -- a runtime index into one array would put it in
@@ -663,8 +668,8 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
             }
         }
     };
-    // step s = (round s / 9, tap s % 9); s >= NH: X chunk s - NH
-    auto load_w = [&](int s, u4 (&rbh)[BIT], u4 (&rbl)[BIT]) __attribute__((always_inline)) {
+    // step s = (round s / SPR, taps TG (s % SPR) ..); s >= NH: X chunk s - NH
+    auto load_w = [&](int s, u4 (&rbh)[BW], u4 (&rbl)[BW]) __attribute__((always_inline)) {
         if constexpr (XF) {
             if (s >= NH) {
                 const int soff = 64 * (xc0 + s - NH);
@@ -676,23 +681,29 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                 return;
             }
         }
-        const int c = chunk_of(s / 9), t = s % 9;
+        const int r = s / SPR, c = chunk_of(r);
         if (c >= cend) return;
-        const int soff = (t * a.Ctot + 32 * c) * 2;
 #pragma unroll
-        for (int it = 0; it < BIT; ++it) {
-            rbh[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwh, bvoff[it], soff, 0));
-            if constexpr (!BF)
-                rbl[it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwl, bvoff[it], soff, 0));
+        for (int u = 0; u < TG; ++u) {
+            const int soff = (((s - SPR * r) * TG + u) * a.Ctot + 32 * c) * 2;
+#pragma unroll
+            for (int it = 0; it < BIT; ++it) {
+                rbh[u * BIT + it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwh, bvoff[it], soff, 0));
+                if constexpr (!BF)
+                    rbl[u * BIT + it] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rwl, bvoff[it], soff, 0));
+            }
         }
     };
-    auto store_w = [&](int stage, const u4 (&rbh)[BIT], const u4 (&rbl)[BIT]) __attribute__((always_inline)) {
-        char* base = ring + stage * BSTAGE;
+    auto store_w = [&](int stage, const u4 (&rbh)[BW], const u4 (&rbl)[BW]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int it = 0; it < BIT; ++it) {
-            const int off = xswz((gt >> 2) + it * (NTG / 4), bq);
-            *(u4*)(base + off) = rbh[it];
-            if constexpr (!BF) *(u4*)(base + BPLANE + off) = rbl[it];
+        for (int u = 0; u < TG; ++u) {
+            char* base = ring + stage * BSTAGE + u * PL * BPLANE;
+#pragma unroll
+            for (int it = 0; it < BIT; ++it) {
+                const int off = xswz((gt >> 2) + it * (NTG / 4), bq);
+                *(u4*)(base + off) = rbh[u * BIT + it];
+                if constexpr (!BF) *(u4*)(base + BPLANE + off) = rbl[u * BIT + it];
+            }
         }
     };
 
@@ -724,22 +735,44 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
     // call site ldx is the set of s's parity (chunk j + 2 goes there), stx the other
     // (chunk j + 1, parked into the other buffer at the end of the step) -- fixed
     // per call site, so no runtime-selected register array (scratch)
-    auto step = [&](int s, u4 (&ldh)[BIT], u4 (&ldl)[BIT], const u4 (&sth)[BIT], const u4 (&stl)[BIT],
+    auto step = [&](int s, u4 (&ldh)[BW], u4 (&ldl)[BW], const u4 (&sth)[BW], const u4 (&stl)[BW],
                     f4 (&ldx)[XIT], f4 (&stx)[XIT]) __attribute__((always_inline)) {
         const bool xs = XF && s >= NH;
-        const int r = s / 9, t = s - 9 * r, j = s - NH;
+        const int r = s / SPR, t = s - SPR * r, j = s - NH;   // t: the step in the round (a tap, or TG taps)
         const int c = chunk_of(r);
         if (s + 2 < nsteps) load_w(s + 2, ldh, ldl);
         if (!xs && t == 0 && chunk_of(r + 1) < cend) load_halo(chunk_of(r + 1));   // in registers until this chunk's taps are done
         if constexpr (XF) {
             if (!xs && t == 0 && r + 1 == nrounds && nx > 0) {   // the last halo round: the first X chunks
-                load_x(0, stx);               // step NH has the parity opposite to s = NH - 9
+                load_x(0, stx);               // step NH has the parity opposite to s = NH - 9 (XF: TG = 1)
                 if (nx > 1) load_x(1, ldx);
             }
             if (xs && j + 2 < nx) load_x(j + 2, ldx);
         }
         if (xs || c < cend) {
             const char* wb = ring + (s & 1) * BSTAGE;
+            if constexpr (BF) {   // TG = 3: kernel row t, its taps (t, u) against ring piece u
+                const int ty = t;
+#pragma unroll
+                for (int u = 0; u < TG; ++u) {
+                    const int tofs = ty * HW2 + u;
+                    const char* wbu = wb + u * BPLANE;
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int ch = 2 * s2 + hsel;
+                        bf16x8 fa[2], fb[2];
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) fa[i] = *(const bf16x8*)(halo + hswz(hb[i] + tofs, hrb[i] + ty, ch));
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj) fb[jj] = *(const bf16x8*)(wbu + xswz(brow0 + 32 * jj, ch));
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+#pragma unroll
+                            for (int jj = 0; jj < 2; ++jj)
+                                acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
+                    }
+                }
+            } else {
             // A fragments: the halo at this tap, or the X buffer at the tile pixel
             const int ty = t / 3;
             const int tofs = ty * HW2 + (t - 3 * ty);
@@ -748,19 +781,6 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const int ch = 2 * s2 + hsel;
-                if constexpr (BF) {
-                    bf16x8 fa[2], fb[2];
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) fa[i] = *(const bf16x8*)(halo + hswz(hb[i] + tofs, hrb[i] + ty, ch));
-#pragma unroll
-                    for (int jj = 0; jj < 2; ++jj) fb[jj] = *(const bf16x8*)(wb + xswz(brow0 + 32 * jj, ch));
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int jj = 0; jj < 2; ++jj)
-                            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
-                    continue;
-                }
                 h8v fah[2], fal[2], fbh[2], fbl[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
@@ -784,13 +804,14 @@ __global__ __launch_bounds__(BM * (BN / 64) * KG, OCC) void conv_h_kernel(ConvAr
                         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[jj], acc[i][jj], 0, 0, 0);
                     }
             }
+            }
         }
-        if (s + 1 < nsteps && (s + 1 >= NH || chunk_of((s + 1) / 9) < cend)) store_w((s + 1) & 1, sth, stl);
+        if (s + 1 < nsteps && (s + 1 >= NH || chunk_of((s + 1) / SPR) < cend)) store_w((s + 1) & 1, sth, stl);
         if constexpr (XF) {
             if (xs && j + 1 < nx) store_x(j + 1, stx);
         }
         __syncthreads();
-        if (!xs && t == 8 && s + 1 < nsteps) {   // every wave is past the last tap of round r
+        if (!xs && t == SPR - 1 && s + 1 < nsteps) {   // every wave is past the last tap of round r
             if (chunk_of(r + 1) < cend) store_halo();
             if constexpr (XF) {
                 if (r + 1 == nrounds && nx > 0) store_x(0, stx);   // step NH: the parity opposite to s = NH - 1
@@ -992,12 +1013,13 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
         const int tw = conv_h_tw(a);
         CFD_REQUIRE(tw > 0 && !a.wlo, CFD_ESHAPE, "conv_h bf16: 3x3 stride-1 with a 16/32/64-divisible width");
         const dim3 g = grid(256, 128);
-        // more than one workgroup per CU (the 128^2 level of config E): the build
-        // whose registers allow 4 waves per SIMD, two workgroups per CU instead of
-        // one (11-30 values spilled, loop-invariant; measured: 128^2 launches 70-88
-        // -> 47 us, config-E forward 5.87 -> 5.47 ms).  Same arithmetic, same bits;
-        // CFD_CONV_KHB_OCC=0 keeps the 3-waves build.
-        static const int occ = getenv("CFD_CONV_KHB_OCC") ? atoi(getenv("CFD_CONV_KHB_OCC")) : 1;
+        // CFD_CONV_KHB_OCC=1: where the grid has more than one workgroup per CU (the
+        // 128^2 level of config E), the build whose registers allow 4 waves per SIMD,
+        // two workgroups per CU (round 4, one tap per step: 128^2 launches 70-88 -> 47
+        // us).  Off since round 5: with three taps per step it spills 49-73 values and
+        // the one-workgroup build runs config E at 4.68 vs 4.99 ms per step (same box).
+        // Same arithmetic, same bits either way.
+        static const int occ = getenv("CFD_CONV_KHB_OCC") ? atoi(getenv("CFD_CONV_KHB_OCC")) : 0;
         if (occ && tw == 64 && (int64_t)g.x * g.y * g.z > 256) {
             if (a.src_bf16)
                 hipLaunchKernelGGL((conv_h_kernel<256, 64, 1, true, true, 128, 4>), g, dim3(512), 0, st, a);

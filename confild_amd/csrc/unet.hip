@@ -726,7 +726,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 // the qkv convolution; in split compute its epilogue also packs K / V
                 conv(xn, at.pre + ".qkv", 3 * at.C, 1, 1, 0, nullptr, nullptr, qb,
                      [&](cfd::ConvArgs& a, const cfd::ConvPlan& plan) {
-                         if (!split_attn || h->compute != CFD_COMPUTE_SPLIT_F16 || !cfd::conv_kv_pack_ok(a, plan, T))
+                         if (!split_attn || h->compute == CFD_COMPUTE_F32 || !cfd::conv_kv_pack_ok(a, plan, T))
                              return;
                          a.kvf = kvws;
                          a.kv_voff = cfd::attention_split_voff(T, at.ch, at.heads, B);

@@ -4,7 +4,7 @@ work is scheduled -- the register-ring depth of the K1s convolution tiles
 CFD_CONV_SMALLN=0 restores 128), the K1h / K1hb split-K 2 run as two
 in-workgroup K groups instead of two workgroups and a partial slab
 (CFD_CONV_KHG: 1 wherever it applies; default 0, never), the K1hb register
-build for two workgroups per CU (CFD_CONV_KHB_OCC, default on above 256
+build for two workgroups per CU (CFD_CONV_KHB_OCC, off by default since round 5; on above 256
 workgroups: the 128^2 batch-5 case), the K1s / K1h epilogues through LDS
 (CFD_CONV_LDSEPI, default on), the attention workgroups of one (sample, head)
 on one XCD (CFD_ATTN_XCD, default on) -- never the tiles' K order or the split-K boundaries, so every
@@ -60,7 +60,7 @@ def _run(env_extra):
 
 
 @pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0", "CFD_CONV_KHG=1",
-                                  "CFD_CONV_KHB_OCC=0", "CFD_CONV_LDSEPI=0", "CFD_ATTN_XCD=0"])
+                                  "CFD_CONV_KHB_OCC=1", "CFD_CONV_LDSEPI=0", "CFD_ATTN_XCD=0"])
 def test_schedule_switch_is_bit_identical(hip, knob):
     # K1h's in-workgroup K groups take no fused skip convolution (conv_takes_skip):
     # that switch is compared with the skip convolutions unfused on both sides
