@@ -52,8 +52,12 @@ __device__ __forceinline__ void split4_mix_x(const f4& x, uint2& hi, uint2& lo) 
 // XF: a fused 1x1 skip convolution (ConvArgs::xsrc1): K tiles past the 3x3 taps'
 // (the "tap" ks * ks) take the raw block input at the output pixel and the skip
 // weights -- [taps | x] as one GEMM, in the same split-K ranges
-template <int BM, int BN, int WGM, int WGN, int KG, int PF = 1, bool XF = false>
+// BF (config E): bf16 operands (the activations rounded RNE as they are staged,
+// weights from the bf16 arena), one v_mfma_f32_32x32x16_bf16 per product, one
+// plane per operand -- the 3x3 convolutions K1hb's halo tiles do not cover (8^2)
+template <int BM, int BN, int WGM, int WGN, int KG, int PF = 1, bool XF = false, bool BF = false>
 __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs a) {
+    static_assert(!(XF && BF), "fused skip convolution: split compute");
     constexpr int NW = WGM * WGN * KG, NT = 64 * NW;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
     constexpr int TM = WTM / 32, TN = WTN / 32;     // 32x32 blocks per wave
@@ -62,7 +66,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
     static_assert(TM >= 1 && TN >= 1 && AIT >= 1 && BIT >= 1, "tile");
     static_assert((BM * KG) % RPP == 0 && (BN * KG) % RPP == 0, "staging");
     constexpr int ABYTES = BM * KG * 64, BBYTES = BN * KG * 64;    // one f16 plane
-    constexpr int STAGE = 2 * ABYTES + 2 * BBYTES;                 // A hi, A lo, B hi, B lo
+    constexpr int PLN = BF ? 1 : 2;                                // planes per operand
+    constexpr int STAGE = PLN * ABYTES + PLN * BBYTES;             // A hi, A lo, B hi, B lo (BF: A, B)
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
     CFD_STAMP(a.stamps, 2, a.seq, 0);
@@ -205,7 +210,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
                 const unsigned voff = kt + g < kt1 ? b_voff[it] : 0x80000000u;
                 const int soff = (tpg[g] * a.Ctot + cbg[g]) * 2;
                 rbh[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwh, voff, soff, 0));
-                rbl[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, voff, soff, 0));
+                if constexpr (!BF)
+                    rbl[set][it] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwl, voff, soff, 0));
             }
         }
 #pragma unroll
@@ -222,20 +228,24 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
         char* base = lds + buf * STAGE;
 #pragma unroll
         for (int it = 0; it < AIT; ++it) {
+            const int off = xswz(a_row[it], kq >> 1) + (kq & 1) * 8;
+            if constexpr (BF) {   // bf16 RNE (v_cvt_pk_bf16_f32), as the K1s bf16 tiles
+                *(bf16x4*)(base + off) = __builtin_convertvector(ra[set][it], bf16x4);
+                continue;
+            }
             uint2 hv, lv;
             if constexpr (XF)
                 split4_mix_x(ra[set][it] * lsc[set][KG == 1 ? 0 : a_g[it]], hv, lv);   // the common scale (exact)
             else
                 split4_mix_x(ra[set][it], hv, lv);
-            const int off = xswz(a_row[it], kq >> 1) + (kq & 1) * 8;
             *(uint2*)(base + off) = hv;
             *(uint2*)(base + ABYTES + off) = lv;
         }
 #pragma unroll
         for (int it = 0; it < BIT; ++it) {
             const int off = xswz(b_row[it], kq >> 1) + (kq & 1) * 8;
-            *(uint2*)(base + 2 * ABYTES + off) = rbh[set][it];
-            *(uint2*)(base + 2 * ABYTES + BBYTES + off) = rbl[set][it];
+            *(uint2*)(base + PLN * ABYTES + off) = rbh[set][it];
+            if constexpr (!BF) *(uint2*)(base + 2 * ABYTES + BBYTES + off) = rbl[set][it];
         }
     };
 
@@ -259,6 +269,19 @@ __global__ __launch_bounds__(64 * WGM * WGN * KG, 1) void conv_x_kernel(ConvArgs
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const int ch = 2 * s + hsel;
+                if constexpr (BF) {
+                    bf16x8 fa[TM], fb[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) fa[i] = *(const bf16x8*)(base + xswz(arow0 + 32 * i, ch));
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) fb[j] = *(const bf16x8*)(base + ABYTES + xswz(brow0 + 32 * j, ch));
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                    continue;
+                }
                 h8v fah[TM], fal[TM], fbh[TN], fbl[TN];
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
@@ -994,8 +1017,7 @@ int conv_h_tw(const ConvArgs& a) {
 }
 
 int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
-    CFD_REQUIRE(a.wbf && (a.wlo || variant == 22 || variant == 26) && !a.tmode, CFD_ESTATE,
-                "conv_x: split-f16 forward only (variants 22 / 26: bf16)");
+    CFD_REQUIRE(a.wbf && !a.tmode, CFD_ESTATE, "conv_x: split-f16 or bf16 forward only");
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_x needs channels % 32 == 0");
     CFD_REQUIRE(splits == 1 || a.part, CFD_ESTATE, "split-K needs a partial buffer");
     {   // K1x / K1h: 32-bit buffer offsets, 24-bit pixel indices
@@ -1101,6 +1123,16 @@ int launch_conv_x(const ConvArgs& a, int variant, int splits, hipStream_t st) {
             else hipLaunchKernelGGL((conv_h_kernel<256, 16>), g, dim3(512), 0, st, a);
         }
         check_launch("conv_h_kernel");
+        return splits;
+    }
+    if (!a.wlo) {   // bf16 operands (config E): the 3x3 convolutions K1hb does not tile
+        CFD_REQUIRE(!a.xsrc1, CFD_ESTATE, "internal: a fused skip convolution needs split compute");
+        switch (variant) {
+            case 1: hipLaunchKernelGGL((conv_x_kernel<128, 128, 2, 2, 1, 1, false, true>), grid(128, 128), dim3(256), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((conv_x_kernel<256, 128, 4, 2, 1, 1, false, true>), grid(256, 128), dim3(512), 0, st, a); break;
+            default: CFD_REQUIRE(false, CFD_EARG, "conv_x variant");
+        }
+        check_launch("conv_x_kernel");
         return splits;
     }
     if (a.xsrc1) {   // fused skip convolution

@@ -2127,7 +2127,11 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
         q.splits = even_splits(nch, q.splits);
         return q;
     }
-    if (kx && a.wbf && a.wlo && !a.tmode && kx_shape && a.Cout >= 128 &&
+    // K1x with bf16 operands (config E's 8^2 3x3 convolutions, which K1hb's 256-pixel
+    // halo tiles do not cover; CFD_CONV_KXB=1, off by default: K1s bf16 tiles)
+    static const int kxb = env_int("CFD_CONV_KXB", 0);   // measured: config E 4.70 vs 4.68 ms per step off (same box)
+    const bool bf_kx = kxb && a.wbf && !a.wlo && a.ks == 3 && a.stride == 1;
+    if (kx && a.wbf && (a.wlo || bf_kx) && !a.tmode && kx_shape && a.Cout >= 128 &&
         srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31)) {
         ConvPlan q;
         // K1h (halo tiles, conv_x.hip) where a 256-pixel block tiles the image
@@ -2136,7 +2140,7 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
         // the config-B 64^2/32^2 shapes, 1.04-1.17x at 16^2 with split-K 8);
         // split-K over the chunks, at least one chunk per split
         static const int kh = env_int("CFD_CONV_KH", 1);
-        if (kh && a.ks == 3 && a.stride == 1 && conv_h_tw(a) > 0) {
+        if (kh && a.wlo && a.ks == 3 && a.stride == 1 && conv_h_tw(a) > 0) {
             q.kx = 20;
             q.bm = 256;
             q.bn = 128;
