@@ -343,6 +343,7 @@ struct Tape {
 struct Sizes {
     size_t max_act = 0, max_qkv = 0, max_cat = 0, max_att = 0;  // floats per sample
     size_t max_kvf = 0;  // split attention's packed K/V fragments (any level)
+    size_t max_abw = 0;  // split attention backward's packs and scales (attention levels)
     std::vector<size_t> hs;                                     // skip-stack tensors, floats per sample
 };
 
@@ -362,6 +363,8 @@ Sizes sizes(const cfd_unet* h) {
         z.max_cat = std::max(z.max_cat, (size_t)hw * hw * (co + cmax));
         z.max_att = std::max(z.max_att, (size_t)hw * hw * co);  // heads * T <= C * T
         z.max_kvf = std::max(z.max_kvf, cfd::attention_split_floats(hw * hw, co));
+        if (has_attn(h, 1 << l) || l == c.n_mult - 1)   // (the middle block attends at the last level)
+            z.max_abw = std::max(z.max_abw, cfd::attention_bwd_split_floats(hw * hw, co));
         for (int r = 0; r < c.num_res_blocks; ++r) z.hs.push_back((size_t)hw * hw * co);
         ch = co;
         if (l != c.n_mult - 1) {
@@ -828,6 +831,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     for (auto& p : gpool) p = ws.take((size_t)B * z.max_cat);
     float* dqkv = ws.take((size_t)B * z.max_qkv);
     float* dd = ws.take((size_t)B * z.max_att);
+    float* abws = ws.take((size_t)B * z.max_abw);
     std::vector<float*> dhs;
     for (size_t n : z.hs) dhs.push_back(ws.take((size_t)B * n));
     // parameter-gradient scratch (pg_ws: sized in the dry walk of cfd_unet_param_grad_workspace_bytes)
@@ -1115,7 +1119,16 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 dconv(dout, at.C, in.H, in.W, at.pre + ".proj_out.weight", at.C, in.H, in.W, 1, 1, 0, 0, dA);
                 cfd::AttnBwdArgs ab{r.qkv, r.o, dA, r.lse, dd, dqkv, T, at.C,
                                     (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
-                cfd::launch_attention_bwd(ab, at.ch, at.heads, B, st);
+                // split compute: K9s (three f16 MFMAs per product); CFD_ATTN_BWD_SPLIT=0
+                // keeps the fp32-MFMA kernels (A/B)
+                static const int abs_on = getenv("CFD_ATTN_BWD_SPLIT") ? atoi(getenv("CFD_ATTN_BWD_SPLIT")) : 1;
+                if (abs_on && h->compute == CFD_COMPUTE_SPLIT_F16 && cfd::attention_bwd_split_ok(T, at.ch)) {
+                    CFD_REQUIRE(cfd::attention_bwd_split_floats(T, at.C) <= z.max_abw, CFD_ESTATE,
+                                "internal: attention backward workspace");
+                    cfd::launch_attention_bwd_split(ab, at.ch, at.heads, B, abws, st);
+                } else {
+                    cfd::launch_attention_bwd(ab, at.ch, at.heads, B, st);
+                }
                 if (pg) {
                     if (r.act1)
                         wgrad(dqkv, 3 * at.C, Act{r.act1, at.C, nullptr, 0, in.H, in.W}, nullptr, 0, in.H, in.W, 1, 1, 0,

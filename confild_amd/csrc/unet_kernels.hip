@@ -476,20 +476,29 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
 // the large latents (config E 128^2) and, with more workgroups than groups, the
 // small batches.
 // ---------------------------------------------------------------------------
-int gn2_chunks(int HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 16)); }
+// Up to 128^2: 256-thread workgroups, up to 64 chunks (config E, B = 1 64^2).
+// Beyond (Case4's 384^2 / 192^2 levels at one chain): 1024-thread workgroups and
+// kGn2BigChunks chunks, so a batch-1 sample still fills the chip (64 KB of loads
+// in flight per CU) and the apply pass reduces the partials in one round of loads
+// (32 lanes per group, kGn2BigChunks / 32 each).
+int gn2_chunks(int HW) {
+    if (HW > kGn2BigHW) return kGn2BigChunks;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 16));
+}
 
-__global__ __launch_bounds__(256) void gn2_stats_kernel(GnArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void gn2_stats_kernel(GnArgs a) {
     const int chunk = blockIdx.x;
     const int64_t b = blockIdx.y;
     const int Ctot = a.Ctot, cq = Ctot / 4, cpg = Ctot / 32;
     const int HW = a.HW, NC = gridDim.x;
     const int p0 = (int)((int64_t)HW * chunk / NC), p1 = (int)((int64_t)HW * (chunk + 1) / NC);
-    const int rows = 256 / cq;
+    const int rows = NT / cq;
     const int q = threadIdx.x % cq, r0 = threadIdx.x / cq;
     const int c0 = 4 * q;
     const bool act = r0 < rows;
     const bool ksrc = a.kpart && c0 < a.C1;
-    __shared__ double red[2][1024];
+    __shared__ double red[2][4 * NT];   // rows * Ctot = 4 * NT
     double s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
     f4 kb = {0.f, 0.f, 0.f, 0.f}, kb2 = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
     if (ksrc) {
@@ -564,17 +573,18 @@ __global__ __launch_bounds__(256) void gn2_stats_kernel(GnArgs a) {
         }
     }
     __syncthreads();
-    // per group: its channels over the rows, fixed order (8 lanes per group, then a
-    // fixed-order combine of the 8)
-    const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
+    // per group: its channels over the rows, fixed order (GL lanes per group, then a
+    // fixed-order combine of the GL)
+    constexpr int GL = NT / 32;
+    const int grp = threadIdx.x / GL, sub = threadIdx.x % GL;
     double ts = 0, ts2 = 0;
-    for (int e = sub; e < rows * cpg; e += 8) {
+    for (int e = sub; e < rows * cpg; e += GL) {
         const int r = e / cpg, c = grp * cpg + (e - r * cpg);
         ts += red[0][r * Ctot + c];
         ts2 += red[1][r * Ctot + c];
     }
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {   // xor butterfly: the same sum on all 8 lanes
+    for (int o = 1; o < GL; o <<= 1) {   // xor butterfly: the same sum on all GL lanes
         ts += __shfl_xor(ts, o);
         ts2 += __shfl_xor(ts2, o);
     }
@@ -585,23 +595,25 @@ __global__ __launch_bounds__(256) void gn2_stats_kernel(GnArgs a) {
     }
 }
 
-__global__ __launch_bounds__(256) void gn2_apply_kernel(GnArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void gn2_apply_kernel(GnArgs a) {
     const int chunk = blockIdx.x;
     const int64_t b = blockIdx.y;
     const int Ctot = a.Ctot, cq = Ctot / 4, cpg = Ctot / 32;
     const int HW = a.HW, NC = gridDim.x;
     __shared__ float ssh[2][1024];
-    {   // the sample's statistics from the chunk partials: 8 lanes per group, every
-        // 8th chunk in chunk order, then an xor butterfly (the same value on every lane)
-        const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
+    {   // the sample's statistics from the chunk partials: GL lanes per group, every
+        // GL-th chunk in chunk order, then an xor butterfly (the same value on every lane)
+        constexpr int GL = NT / 32;
+        const int grp = threadIdx.x / GL, sub = threadIdx.x % GL;
         double S = 0, S2 = 0;
-        for (int k = sub; k < NC; k += 8) {
+        for (int k = sub; k < NC; k += GL) {
             const double2 v = *(const double2*)(a.part + ((b * NC + k) * 32 + grp) * 2);
             S += v.x;
             S2 += v.y;
         }
 #pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
+        for (int o = 1; o < GL; o <<= 1) {
             S += __shfl_xor(S, o);
             S2 += __shfl_xor(S2, o);
         }
@@ -609,8 +621,8 @@ __global__ __launch_bounds__(256) void gn2_apply_kernel(GnArgs a) {
         const double mean = S / n;
         const double var = fmax(S2 / n - mean * mean, 0.0);
         const float mf = (float)mean, rf = (float)(1.0 / sqrt(var + (double)a.eps));
-        if (sub < cpg) {   // this group's channels (cpg <= 32: 8 lanes, a few each)
-            for (int cc = sub; cc < cpg; cc += 8) {
+        if (sub < cpg) {   // this group's channels (cpg <= 32: GL lanes, a few each)
+            for (int cc = sub; cc < cpg; cc += GL) {
                 const int c = grp * cpg + cc;
                 const float sc = rf * a.gamma[c];
                 const float sf = a.beta[c] - mf * sc;
@@ -629,7 +641,7 @@ __global__ __launch_bounds__(256) void gn2_apply_kernel(GnArgs a) {
     }
     __syncthreads();
     const int p0 = (int)((int64_t)HW * chunk / NC), p1 = (int)((int64_t)HW * (chunk + 1) / NC);
-    const int rows = 256 / cq;
+    const int rows = NT / cq;
     const int q = threadIdx.x % cq, r0 = threadIdx.x / cq;
     const int c0 = 4 * q;
     float mx = 0.f;
@@ -715,19 +727,6 @@ __device__ __forceinline__ void split4_mix(const f4& x, uint2& hi, uint2& lo) {
     asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo.y) : "v"(x[3]), "v"(hi.y));
 }
 
-// the K scale of the split attention: q.k scale times log2 e (S in base-2 units)
-__device__ __forceinline__ float kln2(float scale) { return scale * 1.44269504088896340736f; }
-// hi / lo f16 halves of 8 fp32 values (the split attention's fragment operands)
-// (contraction off: v - hi must not fuse with a multiply that formed v in the
-// caller, so the qkv epilogue's K pack and attn_kv_split round identically)
-__device__ __forceinline__ void split8_f16(const float (&v)[8], h8v& hi, h8v& lo) {
-#pragma clang fp contract(off)
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        hi[t] = (_Float16)v[t];
-        lo[t] = (_Float16)(v[t] - (float)hi[t]);
-    }
-}
 
 // SPLIT (MODE 2, default fp32 path): fp32-accurate convolution on f16 MFMA.
 // Activations are split as staged, x = xh + xl (xh = f16(x), xl = f16(x - xh),
@@ -1548,8 +1547,6 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 // v_exp_f32 (ocml's expf is ~11 instructions: the softmax was ~1/3 of the loop's
 // issue) and the saved log-sum-exp is converted back to natural units.
 // ---------------------------------------------------------------------------
-// s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
-constexpr int vmcnt_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
 
 __global__ __launch_bounds__(256) void attn_kv_split_kernel(AttnArgs a, int CH, int heads, int B, h8v* kf,
                                                             h8v* vf) {
@@ -2010,9 +2007,15 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     if (gn2_applies(a)) {
         CFD_REQUIRE(!a.kpart || a.kx, CFD_ESTATE, "internal: gn2 needs the split-K sum's destination");
         a.nchunks = gn2_chunks(a.HW);
-        hipLaunchKernelGGL(gn2_stats_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
-        check_launch("gn2_stats_kernel");
-        hipLaunchKernelGGL(gn2_apply_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
+        if (a.HW > kGn2BigHW) {
+            hipLaunchKernelGGL(gn2_stats_kernel<1024>, dim3(a.nchunks, B), dim3(1024), 0, st, a);
+            check_launch("gn2_stats_kernel");
+            hipLaunchKernelGGL(gn2_apply_kernel<1024>, dim3(a.nchunks, B), dim3(1024), 0, st, a);
+        } else {
+            hipLaunchKernelGGL(gn2_stats_kernel<256>, dim3(a.nchunks, B), dim3(256), 0, st, a);
+            check_launch("gn2_stats_kernel");
+            hipLaunchKernelGGL(gn2_apply_kernel<256>, dim3(a.nchunks, B), dim3(256), 0, st, a);
+        }
         check_launch("gn2_apply_kernel");
         return;
     }

@@ -140,6 +140,12 @@ struct AttnBwdArgs {
     float* dqkv;        // (B, T, 3C)
     int T, C;
     float scale;
+    // split compute (K9s): the packed fragments (attention_bwd_split_floats per
+    // sample) and the per (sample, head, 32-token block) maxima of |dO| and |V|
+    // that fix each (sample, head)'s power-of-two gradient scale; xcdmap as AttnArgs
+    h8v* packs;
+    float* amax;
+    int heads, xcdmap;
 };
 
 struct ConvPlan {
@@ -151,6 +157,11 @@ struct ConvPlan {
 
 constexpr int kGnMaxChunks = 512;
 int gn_chunks(int HW);
+// gn2 (the two-launch full-row GroupNorm) and the DPS GroupNorm backward: pixel
+// chunks of a sample, 1024-thread workgroups beyond kGn2BigHW pixels
+constexpr int kGn2BigHW = 16384, kGn2BigChunks = 256;
+static_assert(kGn2BigChunks <= kGnMaxChunks, "gn2 partials live in the kGnMaxChunks slab");
+int gn2_chunks(int HW);
 // GroupNorm statistics + normalise (+SiLU) into a.out
 void launch_gn(const GnArgs& a, int B, hipStream_t st);
 // whether launch_gn runs the register-resident kernel for this shape (the only
@@ -219,9 +230,32 @@ bool conv_takes_skip(const ConvArgs& a, const ConvPlan& p);
 // backward (unet_vjp.hip)
 int launch_gn_bwd(const GnbArgs& a, int B, hipStream_t st);   // returns the pixel chunks used
 void launch_attention_bwd(const AttnBwdArgs& a, int CH, int heads, int B, hipStream_t st);
+// K9s, the split-f16 attention backward: workspace floats per sample (packs and
+// scales), whether it takes this shape, and the launcher (sets a.packs / a.amax)
+size_t attention_bwd_split_floats(int T, int C);
+bool attention_bwd_split_ok(int T, int CH);
+void launch_attention_bwd_split(const AttnBwdArgs& a, int CH, int heads, int B, float* ws, hipStream_t st);
 void launch_add(float* y, const float* x, int64_t n, hipStream_t st);
 void launch_temb(const int64_t* t, const float* freqs, float* out, int dim, int B, hipStream_t st);
 void launch_linear(const float* x, const float* W, const float* bias, float* y, int B, int K, int N, int act,
                    hipStream_t st);
 
+
+// device helpers shared by the split attention forward (unet_kernels.hip) and
+// its backward (unet_vjp.hip)
+// the K scale of the split attention: q.k scale times log2 e (S in base-2 units)
+__device__ __forceinline__ float kln2(float scale) { return scale * 1.44269504088896340736f; }
+// hi / lo f16 halves of 8 fp32 values (the split attention's fragment operands)
+// (contraction off: v - hi must not fuse with a multiply that formed v in the
+// caller, so the qkv epilogue's K pack and attn_kv_split round identically)
+__device__ __forceinline__ void split8_f16(const float (&v)[8], h8v& hi, h8v& lo) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        hi[t] = (_Float16)v[t];
+        lo[t] = (_Float16)(v[t] - (float)hi[t]);
+    }
+}
+// s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
+constexpr int vmcnt_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
 }  // namespace cfd

@@ -1,0 +1,12 @@
+# round 5k: DPS kernel stats at HEAD (config D one step of 8 chains via kbench, real Case4 20 steps via bench.py)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05k; mkdir -p $O
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_d -o run -- python3 tools/kbench.py dps --batch 8 > $O/d.out 2> $O/d.err || { tail -20 $O/d.err; exit 3; }
+cat $O/d.out
+S=$(find $O/prof_d -name "*kernel_stats.csv" | head -1); cp $S $O/d_stats.csv
+T=$(find $O/prof_d -name "*kernel_trace.csv" | head -1); gzip -c $T > $O/d_trace.csv.gz; rm -rf $O/prof_d
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4 -o run -- python3 bench.py --config Case4 --dps-steps 20 --steps 1 --warmup 1 --no-cpu-baseline > $O/c4.out 2> $O/c4.err || { tail -20 $O/c4.err; exit 4; }
+cat $O/c4.out
+S=$(find $O/prof_c4 -name "*kernel_stats.csv" | head -1); cp $S $O/c4_stats.csv
+T=$(find $O/prof_c4 -name "*kernel_trace.csv" | head -1); gzip -c $T > $O/c4_trace.csv.gz; rm -rf $O/prof_c4
