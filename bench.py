@@ -436,13 +436,16 @@ def b_shards(scaling, world, per_gpu=B):
 # shapes (384^2 latent, channel_mult 1,1,2,2,4,4, SIREN(3,384,3,15,384), 1000 steps)
 # ---------------------------------------------------------------------------
 DPS_CFG = {
-    "D": dict(size=64, channel_mult="", siren=(3, 64, 3, 15, 384), respacing="256", batch=8),
+    "D": dict(size=64, channel_mult="", siren=(3, 64, 3, 15, 384), respacing="256", batch=8, plan_batch=0),
+    # plan_batch: the batch the convolution planner tiles for (cfd_unet_set_plan_batch;
+    # 0 = 8).  One chain per GPU at 384^2: 2 (measured r05o, 30 steps, same box:
+    # 8 -> 50.2, 1 -> 53.5, 2 -> 54.9, 4 -> 54.7 it/s)
     "Case4": dict(size=384, channel_mult="1, 1, 2, 2, 4, 4", siren=(3, 384, 3, 15, 384), respacing="",
-                  batch=1),
+                  batch=1, plan_batch=2),
 }
 
 
-def setup_dps(dev, rank, world, which, batch):
+def setup_dps(dev, rank, world, which, batch, plan_batch=-1):
     """The notebook's objects (inference_phy_random_sensor.ipynb cells 11-20) with
     synthetic weights: guided create_model, a Case4 operator with 10 sensors, 'ps'
     conditioning (scale 1, sigma 0), the 'ddpm' sampler."""
@@ -467,6 +470,7 @@ def setup_dps(dev, rank, world, which, batch):
         m.load_state_dict({k: torch.from_numpy(v) for k, v in
                            synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()}).items()})
         nf.load_state_dict({k: torch.from_numpy(v) for k, v in synth.siren_state_dict(1234, d, L, co, nh, H).items()})
+    m.set_plan_batch(c["plan_batch"] if plan_batch < 0 else plan_batch)
     m.to(dev)
     nf.to(dev)
     cdist.broadcast_module(m)
@@ -685,6 +689,8 @@ def main():
                     help="D / Case4: time this many reverse steps of the loop (0: the whole loop)")
     ap.add_argument("--batch", type=int, default=0,
                     help="A / E: samples per GPU; D / Case4: chains per GPU (0: the config's)")
+    ap.add_argument("--plan-batch", type=int, default=-1,
+                    help="D / Case4: the U-Net planner's nominal batch (-1: the config's; 0: 8)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-gather", action="store_true", help="keep decoded fields on their ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -864,7 +870,7 @@ def main_dps(args, rank, world, dev):
     from confild_amd import synth
     c = DPS_CFG[args.config]
     batch = args.batch or c["batch"]
-    o = setup_dps(dev, rank, world, args.config, batch)
+    o = setup_dps(dev, rank, world, args.config, batch, args.plan_batch)
     smp = o["sampler"]
     nsteps = smp.num_timesteps
     timed = min(args.dps_steps, nsteps) if args.dps_steps else nsteps

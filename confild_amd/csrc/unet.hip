@@ -76,6 +76,7 @@ struct cfd_unet {
     uint16_t* arena_thi = nullptr;  // split compute: f16 hi / lo parts of the scaled input-gradient packs
     uint16_t* arena_tlo = nullptr;
     int compute = CFD_COMPUTE_SPLIT_F16;
+    int plan_b = 0;   // the batch the convolution planner tiles for (0: 8); cfd_unet_set_plan_batch
     int tape_mode = CFD_TAPE_INPUT_VJP;   // what the next forward_tape records
     int tape_mode_rec = CFD_TAPE_INPUT_VJP;   // what the last forward_tape recorded (the replays' layout)
     int* nonfinite = nullptr;  // range guard flag: set by the last convolution on a non-finite eps
@@ -381,7 +382,9 @@ Sizes sizes(const cfd_unet* h) {
 constexpr size_t kSplitPer8 = size_t(16) << 20;
 size_t split_cap(int B) { return kSplitPer8 * (size_t)std::max(1, (B + 7) / 8); }
 
-cfd::ConvPlan plan_checked(const cfd::ConvArgs& a, size_t slab_floats) {
+cfd::ConvPlan plan_checked(const cfd_unet* h, const cfd::ConvArgs& a0, size_t slab_floats) {
+    cfd::ConvArgs a = a0;
+    a.plan_b = h->plan_b;
     const cfd::ConvPlan p = cfd::plan_conv(a, kSplitPer8);
     CFD_REQUIRE(p.splits == 1 || (size_t)p.splits * a.M * a.Cout <= slab_floats, CFD_ESTATE,
                 "internal: split-K slab too small");
@@ -495,6 +498,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         g.Ctot = in.C();
         g.HW = in.H * in.W;
         g.eps = 1e-5f;
+        g.plan_b = h->plan_b;
         g.silu = silu;
         if (pend.splits > 1 && pend.a.out == in.a && pend.a.Cout == in.Ca && cfd::gn_takes_splitk(g, B)) {
             g.kpart = pend.a.part;
@@ -558,7 +562,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         if (!gn_bf16out || h->compute != CFD_COMPUTE_BF16) return false;
         Act n{nbuf, in.C(), nullptr, 0, in.H, in.W};
         const cfd::ConvArgs a = conv_args(n, pre, cout, 3, 1, 0, nullptr, nullptr, nullptr);
-        return a.wbf && !a.wlo && cfd::conv_runs_k1hb(a, plan_checked(a, kSplitCap));
+        return a.wbf && !a.wlo && cfd::conv_runs_k1hb(a, plan_checked(h, a, kSplitCap));
     };
     // tweak: adjusts the launch arguments once the plan is known (the qkv K / V pack);
     // a fused skip convolution (ConvArgs::xsrc1, fuse_skip) is planned as one GEMM
@@ -597,7 +601,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             a.acc_scale = inv_o;
         }
         a.K += x.C();
-        if (!cfd::conv_takes_skip(a, plan_checked(a, kSplitCap))) return false;
+        if (!cfd::conv_takes_skip(a, plan_checked(h, a, kSplitCap))) return false;
         *fa = a;
         return true;
     };
@@ -606,7 +610,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     const cfd::ConvArgs* fused = nullptr) {
         cfd::ConvArgs a = fused ? *fused : conv_args(in, pre, cout, ks, stride, up, embp, resp, out);
         flush();
-        const cfd::ConvPlan plan = plan_checked(a, kSplitCap);
+        const cfd::ConvPlan plan = plan_checked(h, a, kSplitCap);
         if (tweak) tweak(a, plan);
         CFD_REQUIRE(!a.src_bf16 || cfd::conv_runs_k1hb(a, plan), CFD_ESTATE,
                     "internal: bf16 GroupNorm output feeds a convolution other than K1hb at " + pre);
@@ -967,7 +971,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         a.Cout = cout;
         a.M = B * Hout * Wout;
         a.K = ks * ks * cin;
-        cfd::launch_conv(a, plan_checked(a, kSplitCap), st);
+        cfd::launch_conv(a, plan_checked(h, a, kSplitCap), st);
     };
     // with_param (training): the GroupNorm's parameter-gradient partials come out of
     // the same statistics pass (GnbArgs::ppart) and are accumulated into dgamma / dbeta
@@ -991,6 +995,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         g.Ctot = in.C();
         g.HW = in.H * in.W;
         g.silu = silu;
+        g.plan_b = h->plan_b;
         if (with_param && pg) g.ppart = gpp;
         g.amax_out = amax_out;
         const int nch = cfd::launch_gn_bwd(g, B, st);
@@ -1684,6 +1689,15 @@ extern "C" int cfd_unet_set_compute(cfd_unet* h, int compute) {
                     CFD_EARG, "unknown compute mode");
         if (h->compute != compute) ++h->version;
         h->compute = compute;
+    });
+}
+
+extern "C" int cfd_unet_set_plan_batch(cfd_unet* h, int nominal_batch) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(h, CFD_EARG, "null handle");
+        CFD_REQUIRE(nominal_batch >= 0 && nominal_batch <= 64, CFD_EARG, "plan batch must be 0 (default) .. 64");
+        if (h->plan_b != nominal_batch) ++h->version;   // captured graphs hold the old tiles
+        h->plan_b = nominal_batch;
     });
 }
 

@@ -476,14 +476,18 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
 // the large latents (config E 128^2) and, with more workgroups than groups, the
 // small batches.
 // ---------------------------------------------------------------------------
-// Up to 128^2: 256-thread workgroups, up to 64 chunks (config E, B = 1 64^2).
-// Beyond (Case4's 384^2 / 192^2 levels at one chain): 1024-thread workgroups and
-// kGn2BigChunks chunks, so a batch-1 sample still fills the chip (64 KB of loads
-// in flight per CU) and the apply pass reduces the partials in one round of loads
-// (32 lanes per group, kGn2BigChunks / 32 each).
-int gn2_chunks(int HW) {
+// Up to 128^2 at the default planned batch (8): 256-thread workgroups, up to 64
+// chunks (config E, B = 1 64^2); a smaller planned batch (ConvArgs::plan_b, e.g.
+// Case4 at one chain) takes up to 64 * 8 / plan_b (<= 256) chunks.  Beyond 128^2
+// (Case4's 384^2 / 192^2 levels): kGn2BigChunks chunks.  Above 64 chunks the
+// workgroups have 1024 threads (gn2_threads): a batch-1 sample still fills the
+// chip (64 KB of loads in flight per CU) and the apply pass reduces the partials
+// in one round of loads (32 lanes per group, nchunks / 32 each).
+int gn2_chunks(int HW, int plan_b) {
     if (HW > kGn2BigHW) return kGn2BigChunks;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 16));
+    const int pb = plan_b > 0 ? plan_b : 8;
+    const int cap = std::min(kGn2BigChunks, std::max(64, 64 * 8 / pb));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(cap, HW / 16));
 }
 
 template <int NT>
@@ -1981,8 +1985,13 @@ static int env_int(const char* name, int dflt) {
 // per-sample shape only: batch invariance).  CFD_GN2_HW: from this many pixels
 // per sample up (0: never)
 bool gn2_applies(const GnArgs& a) {
-    static const int hw = env_int("CFD_GN2_HW", 4096);   // measured: B = 1 64^2 -3.5 %, config E -3 %, B = 8 flat
-    return hw > 0 && a.HW >= hw && a.Ctot % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0 && a.Ctot <= 1024;
+    // measured: B = 1 64^2 -3.5 %, config E -3 %, B = 8 flat; the threshold scales
+    // with the planned batch (plan_b 2: from 1024 pixels, where the one-launch
+    // kernels' 32 workgroups per sample leave a batch-1 chip idle)
+    static const int hw = env_int("CFD_GN2_HW", 4096);
+    const int pb = a.plan_b > 0 ? a.plan_b : 8;
+    return hw > 0 && (int64_t)a.HW * 8 >= (int64_t)hw * pb && a.Ctot % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0 &&
+           a.Ctot <= 1024;
 }
 
 bool gn_takes_splitk(const GnArgs& a, int B) {
@@ -2006,8 +2015,8 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     CFD_REQUIRE(!a.kpart || gn_takes_splitk(a, B), CFD_ESTATE, "internal: split-K source on a GroupNorm path without it");
     if (gn2_applies(a)) {
         CFD_REQUIRE(!a.kpart || a.kx, CFD_ESTATE, "internal: gn2 needs the split-K sum's destination");
-        a.nchunks = gn2_chunks(a.HW);
-        if (a.HW > kGn2BigHW) {
+        a.nchunks = gn2_chunks(a.HW, a.plan_b);
+        if (gn2_threads(a.nchunks) == 1024) {
             hipLaunchKernelGGL(gn2_stats_kernel<1024>, dim3(a.nchunks, B), dim3(1024), 0, st, a);
             check_launch("gn2_stats_kernel");
             hipLaunchKernelGGL(gn2_apply_kernel<1024>, dim3(a.nchunks, B), dim3(1024), 0, st, a);
@@ -2074,7 +2083,10 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     static const int force_bm = env_int("CFD_CONV_BM", 0);
     static const int target = env_int("CFD_CONV_TARGET_WG", 768);
     // development: CFD_PLAN_B plans for that batch instead of 8 (small-batch experiments)
-    static const int plan_b = env_int("CFD_PLAN_B", 8);
+    static const int plan_b_env = env_int("CFD_PLAN_B", 8);
+    const int plan_b = a.plan_b > 0 ? a.plan_b : plan_b_env;
+    // the split-K slab guard at the planned batch (part_cap_floats is per 8 samples)
+    part_cap_floats = part_cap_floats / 8 * (size_t)plan_b;
     ConvPlan p;
     const int64_t mn = (int64_t)plan_b * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;
@@ -2103,6 +2115,14 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     // memory guard, on the nominal shape too: part_cap_floats is the slab per 8
     // samples (the caller sizes the real slab as ceil(B/8) of these)
     while (p.splits > 1 && (size_t)p.splits * mn * a.Cout > part_cap_floats) p.splits /= 2;
+    // the large-latent levels (Case4's 192^2 / 384^2) with <= 128 input channels:
+    // K1s 128x128 tiles of 8 waves (tools/convbench at one sample: 384^2 128->128
+    // 178 vs K1h 199 us, the 2x upsampling 174 vs 197, 192^2 128->128 63 vs 74;
+    // 256 input channels stay on K1h: 344 vs 364 us)
+    static const int k1s_big = env_int("CFD_CONV_K1S_HW", 36864);
+    if (k1s_big > 0 && a.wlo && a.ks == 3 && a.stride == 1 && !a.tmode && a.Ctot <= 128 &&
+        (int64_t)a.Hout * a.Wout >= k1s_big)
+        return p;
     // K1x (conv_x.hip) for the split-f16 3x3 stride-1 convolutions: 64x64 wave
     // tiles on 32x32x16 MFMAs; 256x128 workgroup tiles where the per-sample shape
     // has >= 256 pixels at batch 8, 128x128 / 4 waves below (tools/convbench:

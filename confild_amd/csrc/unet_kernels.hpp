@@ -40,6 +40,9 @@ struct GnArgs {
     // atomicMax of the float bits per workgroup -- the operand range the split
     // weight gradients of the next convolution need
     unsigned* amax_out;
+    // the model's planned batch (ConvArgs::plan_b; 0: 8): gn2's chunk count and
+    // reach, a function of the per-sample shape and this setting only
+    int plan_b;
 };
 
 struct ConvArgs {
@@ -89,6 +92,10 @@ struct ConvArgs {
     float main_scale, x_scale;
     unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
     int seq;                      // launch sequence number (timestamps)
+    // the batch plan_conv tiles for (0: 8, or CFD_PLAN_B): a per-model setting
+    // (cfd_unet_set_plan_batch), never the real batch, so a sample's sums do not
+    // depend on the batch it runs in
+    int plan_b;
 };
 // development: the timestamp buffer the CFD_STAMPS build's kernels write (null: off)
 void stamps_set(unsigned long long* buf);
@@ -128,6 +135,7 @@ struct GnbArgs {
     // with one atomicMax of the float bits per workgroup (a zeroed slot)
     unsigned* amax_out;
     int C1, C2, Ctot, HW, silu, nchunks, B;
+    int plan_b;   // the model's planned batch (0: 8), as GnArgs::plan_b
 };
 
 // QKVAttentionLegacy backward (flash-style, recomputes P from the saved LSE).
@@ -161,7 +169,10 @@ int gn_chunks(int HW);
 // chunks of a sample, 1024-thread workgroups beyond kGn2BigHW pixels
 constexpr int kGn2BigHW = 16384, kGn2BigChunks = 256;
 static_assert(kGn2BigChunks <= kGnMaxChunks, "gn2 partials live in the kGnMaxChunks slab");
-int gn2_chunks(int HW);
+int gn2_chunks(int HW, int plan_b);
+// gn2's workgroup size for nchunks chunks: 1024 threads beyond 64 (the apply pass
+// then reduces the chunk partials with 32 lanes per group, nchunks / 32 loads each)
+inline int gn2_threads(int nchunks) { return nchunks > 64 ? 1024 : 256; }
 // GroupNorm statistics + normalise (+SiLU) into a.out
 void launch_gn(const GnArgs& a, int B, hipStream_t st);
 // whether launch_gn runs the register-resident kernel for this shape (the only

@@ -233,6 +233,7 @@ class UNetModel(nn.Module):
         # convolution arithmetic: "split_f16" (default; fp32-accurate on f16 MFMA, DESIGN.md
         # K1s), "fp32" (exact fp32 MFMA) or "bf16" (bf16 operands, config E)
         self.compute = "split_f16"
+        self.plan_batch = 0     # the batch the convolution planner tiles for (0: 8)
         self._handles = {}      # device index -> (handle ptr, uploaded signature)
         self._workspaces = {}   # (device, B) -> uint8 tensor
 
@@ -286,6 +287,15 @@ class UNetModel(nn.Module):
         self.compute = compute
         return self
 
+    def set_plan_batch(self, nominal_batch: int):
+        """The batch the convolution planner tiles for (0: the default 8): a per-model
+        setting, so results stay bit-identical across the batches a sample runs in.
+        Set it near the chains per GPU when that is far from 8 (cfd_unet_set_plan_batch)."""
+        if not 0 <= int(nominal_batch) <= 64:
+            raise ValueError("plan batch must be in 0..64")
+        self.plan_batch = int(nominal_batch)
+        return self
+
     def _signature(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
@@ -314,6 +324,7 @@ class UNetModel(nn.Module):
             _lib.check(lib.cfd_unet_ready(h), "cfd_unet_ready")
             entry[1] = sig
         _lib.check(lib.cfd_unet_set_compute(entry[0], self.COMPUTE_MODES[self.compute]), "cfd_unet_set_compute")
+        _lib.check(lib.cfd_unet_set_plan_batch(entry[0], self.plan_batch), "cfd_unet_set_plan_batch")
         return entry[0]
 
     def _workspace(self, h, device, B):

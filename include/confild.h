@@ -99,6 +99,12 @@ int  cfd_unet_workspace_bytes(const cfd_unet* h, int B, size_t* bytes);
 #define CFD_COMPUTE_BF16      1
 #define CFD_COMPUTE_SPLIT_F16 2
 int  cfd_unet_set_compute(cfd_unet* h, int compute);
+/* The batch the convolution planner tiles for (tiles, split-K counts, kernel
+ * family): 0 = 8 (default).  A per-model setting, never the real batch, so a
+ * sample's eps stays bit-identical whatever batch or GPU it runs in; set it to
+ * the chains a GPU runs when that is far from 8 (real Case4 at one chain: 2,
+ * +8 % steps/s).  No reference counterpart (a performance setting). */
+int  cfd_unet_set_plan_batch(cfd_unet* h, int nominal_batch);
 int  cfd_unet_forward(cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                       void* workspace, size_t ws_bytes, void* stream);
 /* Range guard of the split-f16 compute (no reference counterpart: the

@@ -63,8 +63,15 @@ static const Shape SHAPES[] = {
     {"L2 qkv 384->1152", 8, 16, 16, 384, 0, 1152, 1, 1, 0},
     {"L1 qkv 256->768", 8, 32, 32, 256, 0, 768, 1, 1, 0},
     {"C4 384^2 conv 128->128", 1, 384, 384, 128, 0, 128, 3, 1, 0},
+    {"C4 384^2 conv 256->128", 1, 384, 384, 256, 0, 128, 3, 1, 0},
+    {"C4 384^2 conv 128->256", 1, 384, 384, 128, 0, 256, 3, 1, 0},
+    {"C4 384^2 up 128 (192->384)", 1, 192, 192, 128, 0, 128, 3, 1, 1},
+    {"C4 192^2 conv 128->128", 1, 192, 192, 128, 0, 128, 3, 1, 0},
+    {"C4 192^2 conv 256->128", 1, 192, 192, 256, 0, 128, 3, 1, 0},
     {"C4 96^2 conv 256->256", 1, 96, 96, 256, 0, 256, 3, 1, 0},
+    {"C4 96^2 conv 512->256", 1, 96, 96, 512, 0, 256, 3, 1, 0},
     {"C4 48^2 conv 256->256", 1, 48, 48, 256, 0, 256, 3, 1, 0},
+    {"C4 48^2 conv 512->256", 1, 48, 48, 512, 0, 256, 3, 1, 0},
 };
 
 static uint16_t f2h(float v) {
@@ -79,7 +86,17 @@ static float h2f(uint16_t u) {
     return (float)h;
 }
 
+static int bench_main(int argc, char** argv);
 int main(int argc, char** argv) {
+    try {
+        return bench_main(argc, argv);
+    } catch (const cfd::Error& e) {
+        fprintf(stderr, "cfd::Error %d: %s\n", e.code, e.msg.c_str());
+        return 2;
+    }
+}
+
+static int bench_main(int argc, char** argv) {
     std::vector<int> variants;
     for (int i = 1; i < argc; ++i) variants.push_back(atoi(argv[i]));
     if (variants.empty()) variants = {1, 2, 20};   // the K1x and K1h variants the planner ships (round 3)
