@@ -28,6 +28,7 @@ struct cfd_sampler {
     int64_t* tbuf = nullptr;        // (2, B): this step's table index / model timestep per sample
     cfd::SamplerCtl* ctl = nullptr;
     void* ws = nullptr;             // U-Net workspace
+    size_t ws_bytes = 0;            // (re-sized when the model's planned batch grows its split-K slab)
     // captured graphs: [0] one step, [1] `unroll` steps, and the U-Net handle version
     // they were captured at (a set_param can change a weight's split scale, which
     // is a kernel argument; set_compute changes the kernels)
@@ -113,7 +114,8 @@ extern "C" int cfd_sampler_create(const cfd_unet* unet, const cfd_sched* sched, 
             CFD_HIP(hipMalloc(&sp->tseq, sizeof(int64_t) * 2 * (size_t)n_steps));
             CFD_HIP(hipMalloc(&sp->tbuf, sizeof(int64_t) * 2 * (size_t)B));
             CFD_HIP(hipMalloc(&sp->ctl, sizeof(cfd::SamplerCtl)));
-            CFD_HIP(hipMalloc(&sp->ws, cfd::unet_ws_bytes(unet, B)));
+            sp->ws_bytes = cfd::unet_ws_bytes(unet, B);
+            CFD_HIP(hipMalloc(&sp->ws, sp->ws_bytes));
             CFD_HIP(hipMemcpy(sp->tseq, host_tidx, sizeof(int64_t) * n_steps, hipMemcpyHostToDevice));
             CFD_HIP(hipMemcpy(sp->tseq + n_steps, host_tmodel, sizeof(int64_t) * n_steps, hipMemcpyHostToDevice));
         } catch (...) {
@@ -145,6 +147,17 @@ extern "C" int cfd_sampler_run(cfd_sampler* sp, const float* x_in, float* x_out,
         cfd::unet_check_ready(sp->unet);
         cfd::DeviceGuard dg(sp->device);
         const hipStream_t st = (hipStream_t)stream;
+        if (const size_t need = cfd::unet_ws_bytes(sp->unet, sp->B); need > sp->ws_bytes) {
+            // the model's planned batch changed (cfd_unet_set_plan_batch): a larger
+            // slab, and graphs that captured the old workspace pointer are stale
+            CFD_HIP(hipDeviceSynchronize());
+            destroy_graphs(sp);
+            CFD_HIP(hipFree(sp->ws));
+            sp->ws = nullptr;
+            sp->ws_bytes = 0;
+            CFD_HIP(hipMalloc(&sp->ws, need));
+            sp->ws_bytes = need;
+        }
         const size_t bytes = sizeof(float) * (size_t)sp->B * sp->n_per_sample;
         if (x_in) CFD_HIP(hipMemcpyAsync(sp->x, x_in, bytes, hipMemcpyDeviceToDevice, st));
         cfd::launch_sampler_set(sp->ctl, (uint64_t)k0, seed, offset / 4, st);

@@ -377,14 +377,24 @@ Sizes sizes(const cfd_unet* h) {
     return z;
 }
 
-// split-K partial slab: plan_conv keeps splits * (8 samples' M x N) within
-// kSplitPer8 floats, so a slab of ceil(B/8) of those always suffices
+// split-K partial slab
 constexpr size_t kSplitPer8 = size_t(16) << 20;
-size_t split_cap(int B) { return kSplitPer8 * (size_t)std::max(1, (B + 7) / 8); }
+// the batch the convolution planner and gn2 tile for: the model's setting
+// (cfd_unet_set_plan_batch), else CFD_PLAN_B (development), else 8
+int plan_batch(const cfd_unet* h) {
+    static const int env = getenv("CFD_PLAN_B") ? std::max(1, atoi(getenv("CFD_PLAN_B"))) : 8;
+    return h->plan_b > 0 ? h->plan_b : env;
+}
+// (kSplitPer8 per planned batch: plan_conv keeps splits * (plan_b samples' M x N)
+// within it, so ceil(B / plan_b) of those cover any real batch)
+size_t split_cap(const cfd_unet* h, int B) {
+    const int pb = plan_batch(h);
+    return kSplitPer8 * (size_t)std::max(1, (B + pb - 1) / pb);
+}
 
 cfd::ConvPlan plan_checked(const cfd_unet* h, const cfd::ConvArgs& a0, size_t slab_floats) {
     cfd::ConvArgs a = a0;
-    a.plan_b = h->plan_b;
+    a.plan_b = plan_batch(h);
     const cfd::ConvPlan p = cfd::plan_conv(a, kSplitPer8);
     CFD_REQUIRE(p.splits == 1 || (size_t)p.splits * a.M * a.Cout <= slab_floats, CFD_ESTATE,
                 "internal: split-K slab too small");
@@ -400,7 +410,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     const int mc = c.model_channels, S = c.image_size;
     const Sizes z = sizes(h);
     const bool launch = launch_req && !ws.dry && !(tape && tape->tws->dry);
-    const size_t kSplitCap = split_cap(B);
+    const size_t kSplitCap = split_cap(h, B);
     float* temb = tape ? tape->tws->take((size_t)B * mc) : ws.take((size_t)B * mc);
     float* h1 = tape ? tape->tws->take((size_t)B * h->tdim) : ws.take((size_t)B * h->tdim);
     float* emb = tape ? tape->tws->take((size_t)B * h->tdim) : ws.take((size_t)B * h->tdim);
@@ -498,7 +508,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         g.Ctot = in.C();
         g.HW = in.H * in.W;
         g.eps = 1e-5f;
-        g.plan_b = h->plan_b;
+        g.plan_b = plan_batch(h);
         g.silu = silu;
         if (pend.splits > 1 && pend.a.out == in.a && pend.a.Cout == in.Ca && cfd::gn_takes_splitk(g, B)) {
             g.kpart = pend.a.part;
@@ -827,7 +837,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
     const auto& c = h->cfg;
     const int S = c.image_size;
     const Sizes z = sizes(h);
-    const size_t kSplitCap = split_cap(B);
+    const size_t kSplitCap = split_cap(h, B);
     float* splitk = ws.take(kSplitCap);
     double* gnpart = (double*)ws.take((size_t)B * cfd::kGnMaxChunks * 32 * 2 * 2);
     float* gnfin = ws.take((size_t)B * 64);
@@ -995,7 +1005,7 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
         g.Ctot = in.C();
         g.HW = in.H * in.W;
         g.silu = silu;
-        g.plan_b = h->plan_b;
+        g.plan_b = plan_batch(h);
         if (with_param && pg) g.ppart = gpp;
         g.amax_out = amax_out;
         const int nch = cfd::launch_gn_bwd(g, B, st);
@@ -1696,7 +1706,10 @@ extern "C" int cfd_unet_set_plan_batch(cfd_unet* h, int nominal_batch) {
     return cfd::guard([&] {
         CFD_REQUIRE(h, CFD_EARG, "null handle");
         CFD_REQUIRE(nominal_batch >= 0 && nominal_batch <= 64, CFD_EARG, "plan batch must be 0 (default) .. 64");
-        if (h->plan_b != nominal_batch) ++h->version;   // captured graphs hold the old tiles
+        if (h->plan_b != nominal_batch) {
+            ++h->version;          // captured graphs hold the old tiles
+            h->ws_cache.clear();   // the split-K slab is sized per planned batch
+        }
         h->plan_b = nominal_batch;
     });
 }

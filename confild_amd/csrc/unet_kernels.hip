@@ -2084,9 +2084,9 @@ ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
     static const int target = env_int("CFD_CONV_TARGET_WG", 768);
     // development: CFD_PLAN_B plans for that batch instead of 8 (small-batch experiments)
     static const int plan_b_env = env_int("CFD_PLAN_B", 8);
+    // part_cap_floats: the split-K slab per planned batch (the caller sizes the real
+    // slab as ceil(B / plan_b) of these)
     const int plan_b = a.plan_b > 0 ? a.plan_b : plan_b_env;
-    // the split-K slab guard at the planned batch (part_cap_floats is per 8 samples)
-    part_cap_floats = part_cap_floats / 8 * (size_t)plan_b;
     ConvPlan p;
     const int64_t mn = (int64_t)plan_b * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;

@@ -181,7 +181,7 @@ bool gn_takes_splitk(const GnArgs& a, int B);
 // whether launch_gn runs the two-launch full-row form (gn2_*) for this shape: it
 // then needs GnArgs::kx for a split-K source (the apply pass re-reads the sum)
 bool gn2_applies(const GnArgs& a);
-// part_cap_floats: split-K slab available per 8 samples (plans depend on the
+// part_cap_floats: split-K slab available per planned batch (ConvArgs::plan_b) (plans depend on the
 // per-sample shape only, never on the batch)
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats);
 // Returns the split count.  With defer and splits > 1 the reduction is not

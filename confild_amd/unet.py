@@ -293,6 +293,10 @@ class UNetModel(nn.Module):
         Set it near the chains per GPU when that is far from 8 (cfd_unet_set_plan_batch)."""
         if not 0 <= int(nominal_batch) <= 64:
             raise ValueError("plan batch must be in 0..64")
+        if int(nominal_batch) != self.plan_batch:
+            # the workspaces hold the split-K slab, sized per planned batch
+            self._workspaces = {}
+            self._vjp_ws, self._vjp_key = None, None
         self.plan_batch = int(nominal_batch)
         return self
 

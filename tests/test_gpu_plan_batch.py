@@ -54,3 +54,20 @@ def test_plan_batch_rejects_out_of_range(hip):
     m = _model(32, "1,2,3,4")
     with pytest.raises(ValueError):
         m.set_plan_batch(65)
+
+
+def test_plan_batch_change_resizes_native_loop(hip):
+    """A native sampling loop created at one planned batch keeps working after the
+    model's planned batch changes (the split-K slab in its workspace grows; its
+    graphs are recaptured), and the chains still shard bit-exactly."""
+    from confild_amd.script_util import create_gaussian_diffusion
+    m = _model(64, "")
+    d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="6")
+    shape = (2, 1, 64, 64)
+    a = d.p_sample_loop(m, shape, seed=5)
+    m.set_plan_batch(2)
+    b = d.p_sample_loop(m, shape, seed=5)
+    one = d.p_sample_loop(m, (1, 1, 64, 64), seed=5, sample_offset=1)
+    assert torch.equal(one, b[1:2])
+    assert torch.isfinite(b).all()
+    assert float((a - b).abs().max()) < 1e-3 * max(1.0, float(a.abs().max()))

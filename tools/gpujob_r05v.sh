@@ -8,7 +8,7 @@ for e in "X=0" "CFD_GNB2=2" "X=0"; do
   env $e timeout -k 10 200 python3 tools/kbench.py dps --batch 8 > $O/d.out 2> $O/d.err || { tail -20 $O/d.err; exit 5; }
   echo "$e $(python3 -c "import json; d=json.load(open('$O/d.out')); print(round(d['step_ms'],3), round(d['unet_vjp_ms'],3))")"
 done
-for pb in 2 0 2 0; do
+for pb in 2 1 0 2 1; do
   timeout -k 10 200 python3 bench.py --config Case4 --dps-steps 30 --steps 1 --warmup 1 --no-cpu-baseline --plan-batch $pb > $O/c4ab.json 2> $O/c4ab.err || { tail -20 $O/c4ab.err; exit 8; }
   python3 -c "import json; d=json.load(open('$O/c4ab.json')); print('pb=$pb', round(d['value'],3), round(d['ms_per_step'],3))"
 done
