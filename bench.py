@@ -203,7 +203,7 @@ def gather_to_root(x, dim, sizes, world):
 # ---------------------------------------------------------------------------
 # config B: sample -> de-normalise -> decode
 # ---------------------------------------------------------------------------
-def setup_B(dev, rank, world, siren_compute, unet_compute):
+def setup_B(dev, rank, world, siren_compute, unet_compute, plan_batch=0):
     from confild_amd import dist as cdist
     from confild_amd import synth
     from confild_amd.nf_networks import SIRENAutodecoder_film
@@ -223,6 +223,9 @@ def setup_B(dev, rank, world, siren_compute, unet_compute):
     cdist.broadcast_module(model)
     cdist.broadcast_module(nf)
     model.set_compute(unet_compute)
+    # the default planned batch (8): the weak-scaling batch per GPU, and the same
+    # plan for the strong-scaling shards, so a sample's bits never depend on N
+    model.set_plan_batch(max(plan_batch, 0))
     nf.set_compute(siren_compute)
     diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=STEPS)
     ax = torch.linspace(0, 1, GRID)
@@ -267,10 +270,10 @@ def step_B(o, dev, seed, start, count, ev=None):
 UNCOND_CFG = {
     "A": dict(size=32, channel_mult="1,2,3,4", respacing="ddim50", ddim=True, batch=1,
               siren=dict(d=2, L=32, c=3, nh=10, H=128), coords=1000, unet="split_f16",
-              gflops=19.23),
+              gflops=19.23, plan_batch=0),
     "E": dict(size=128, channel_mult="", respacing="", ddim=False, batch=8,
               siren=dict(d=2, L=128, c=2, nh=17, H=256), coords=256 * 256, unet="bf16",
-              gflops=140.75),
+              gflops=140.75, plan_batch=0),
 }
 
 
@@ -296,6 +299,7 @@ def main_uncond(args, rank, world, dev):
     cdist.broadcast_module(model)
     cdist.broadcast_module(nf)
     model.set_compute(c["unet"] if args.unet_compute == "split_f16" else args.unet_compute)
+    model.set_plan_batch(c["plan_batch"] if args.plan_batch < 0 else args.plan_batch)
     nf.set_compute(args.siren_compute)
     diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=c["respacing"])
     nsteps = diff.num_timesteps
@@ -690,7 +694,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0,
                     help="A / E: samples per GPU; D / Case4: chains per GPU (0: the config's)")
     ap.add_argument("--plan-batch", type=int, default=-1,
-                    help="D / Case4: the U-Net planner's nominal batch (-1: the config's; 0: 8)")
+                    help="A / B / D / E / Case4: the U-Net planner's nominal batch (-1: the config's; 0: 8)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-gather", action="store_true", help="keep decoded fields on their ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -723,7 +727,7 @@ def main():
     if args.config in ("A", "E"):
         return main_uncond(args, rank, world, dev)
     if args.config == "B":
-        o = setup_B(dev, rank, world, args.siren_compute, args.unet_compute)
+        o = setup_B(dev, rank, world, args.siren_compute, args.unet_compute, args.plan_batch)
         nf = o["nf"]
         shards = b_shards(args.scaling, world, args.per_gpu_batch or B)
         glob = sum(cnt for _, cnt in shards)
