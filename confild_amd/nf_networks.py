@@ -148,6 +148,22 @@ class SIRENAutodecoder_film(nn.Module):
         b = latents.shape[0] if latents.dim() >= 2 else 1
         return coords.reshape(-1, d), latents.reshape(b, L), spatial
 
+    def _dev_param(self, t, dev):
+        """fp32 device copy of a (usually host) normaliser parameter, cached while the
+        source tensor is unchanged: a host-to-device copy from pageable memory waits for
+        the stream, which in the DPS step would idle the GPU between the U-Net forward
+        and the SIREN tape (4 such copies per step before the cache)."""
+        if t.device == dev and t.dtype == torch.float32:
+            return t
+        cache = self.__dict__.setdefault("_norm_dev_cache", {})
+        key = (id(t), dev)
+        hit = cache.get(key)
+        if hit is not None and hit[0] is t and hit[1] == t._version:
+            return hit[2]
+        v = t.to(device=dev, dtype=torch.float32)
+        cache[key] = (t, t._version, v)
+        return v
+
     def _norm_args(self, cf, N, dev, x_normalizer, y_normalizer):
         """Fusable '-11' normaliser bounds -> (coords, xmax, xmin, ymax, ymin, ystride, post)."""
         d, c = self.in_coord_features, self.out_features
@@ -157,8 +173,8 @@ class SIRENAutodecoder_film(nn.Module):
             if x_normalizer.method != "-11":
                 cf = x_normalizer.normalize(cf).contiguous()
             else:
-                xmax = x_normalizer.params[0].to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
-                xmin = x_normalizer.params[1].to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+                xmax = self._dev_param(x_normalizer.params[0], dev).reshape(-1).contiguous()
+                xmin = self._dev_param(x_normalizer.params[1], dev).reshape(-1).contiguous()
                 if xmax.numel() != d:
                     raise ValueError("coordinate normaliser must have one (max, min) per coordinate feature")
         post = None
@@ -166,8 +182,8 @@ class SIRENAutodecoder_film(nn.Module):
             if y_normalizer.method != "-11":
                 post = y_normalizer
             else:
-                ymax = y_normalizer.params[0].to(device=dev, dtype=torch.float32)
-                ymin = y_normalizer.params[1].to(device=dev, dtype=torch.float32)
+                ymax = self._dev_param(y_normalizer.params[0], dev)
+                ymin = self._dev_param(y_normalizer.params[1], dev)
                 if ymax.numel() == c:
                     ystride = 0
                 elif ymax.numel() == N * c:

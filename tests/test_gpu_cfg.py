@@ -269,6 +269,50 @@ def test_configD_batched_chains_equal_single_chains(hip):
         assert torch.equal(sampler.distances[:, 0], dfull[:, s]), s
 
 
+def test_configD_dps_chain_vs_oracle(hip):
+    """Config D widths, 12 consecutive guided steps (indices 30 .. 19 of the 256-step
+    loop), each from the HIP path's own previous image, against the CPU oracle's
+    autograd chain from the same start and noise (oracle/dps.py, itself pinned to
+    the reference's steps at these widths by test_oracle_configD_dps_steps).  Per
+    step image <= 1e-4 of the latent scale and residual norm <= 1e-4 relative; the
+    chain's drift stays at that level (no chaotic growth)."""
+    from confild_amd.guided.unet import create_model as guided_model
+    from oracle import diffusion as od
+    from oracle import dps as odps
+    from oracle import unet as ou
+    c = DPS_D
+    g = golden("golden_dpsD.npz")
+    model = _unet(c, guided_model)
+    op = _operator_D(g)
+    cond, sampler = _guided(c["respacing"], op, c["scale"])
+    y = torch.from_numpy(g["measurement"])
+    S, L = c["unet"]["image_size"], c["siren"][1]
+    cfg = ou.Config(**c["unet"])
+    sd = {k: torch.from_numpy(v) for k, v in unet_weights(ou.param_shapes(cfg), c["seed"]).items()}
+    dd, _, co, nh, H = c["siren"]
+    ssd = {k: torch.from_numpy(v) for k, v in synth.siren_state_dict(c["siren_seed"], dd, L, co, nh, H).items()}
+    T = lambda k: torch.from_numpy(g[k])  # noqa: E731
+    operator = lambda x0: odps.case4_forward(ssd, T("coords"), T("xhi"), T("xlo"), T("yhi"), T("ylo"),  # noqa: E731
+                                             T("vmax"), T("vmin"), x0, batch=16)
+    unet = lambda x, t: ou.forward(sd, cfg, x, t)  # noqa: E731
+    tb = od.Tables(1000, "cosine", c["respacing"])
+    x_ref = torch.from_numpy(synth.normal(c["siren_seed"], "dpsD/chain_x", (1, 1, S, L)))
+    x_hip = x_ref.to(DEV)
+    worst = 0.0
+    for k, idx in enumerate(range(30, 18, -1)):
+        nz = torch.from_numpy(noise_for(f"{c['tag']}/chain", k, (1, 1, S, L)))
+        x_ref, _, _, norm_ref = odps.dps_step(tb, unet, operator, x_ref, idx, y, nz, c["scale"])
+        out = sampler.p_sample_step(model, x_hip, idx, y.to(DEV), cond.conditioning, noise=nz.to(DEV))
+        x_hip = out["sample"]
+        lat = max(1.0, float(x_ref.abs().max()))
+        err = float((x_hip.cpu() - x_ref).abs().max()) / lat
+        en = abs(float(out["distance"][0]) - float(norm_ref)) / float(norm_ref)
+        worst = max(worst, err)
+        print(f"config D chain step {idx}: image {err:.2e}, norm rel {en:.2e}")
+        assert err <= 1e-4 and en <= 1e-4, (idx, err, en)
+    assert worst <= 1e-4
+
+
 def _case4_operator(tmp):
     from confild_amd.guided.measurements import get_operator
     paths = case4_files(str(tmp))
