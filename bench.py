@@ -240,6 +240,80 @@ def setup_B(dev, rank, world, siren_compute, unet_compute, plan_batch=0):
     return dict(model=model, diff=diff, nf=nf, coords=coords, xn=xn, yn=yn, vmax=vmax, vmin=vmin)
 
 
+def sample_B(o, dev, seed, start, count):
+    """This rank's samples of one batch: the 256-step loop, then de-normalised."""
+    from confild_amd import _lib
+    lat = o["diff"].p_sample_loop(o["model"], (count, 1, S, S), seed=seed, sample_offset=start)[:, 0]
+    den = torch.empty_like(lat)
+    _lib.check(_lib.load().cfd_latent_denorm(_lib.ptr(lat), _lib.ptr(den), lat.numel(), _lib.ptr(o["vmax"]),
+                                             _lib.ptr(o["vmin"]), 1, _lib.stream_of(dev)), "denorm")
+    return den
+
+
+class PipelineB:
+    """Config B as a two-stage pipeline over the chip's two CU halves
+    (cfd_stream_create_cu_range): the decode of batch k-1 runs on one half while
+    batch k is sampled on the other; the first batch samples on the whole chip.
+    Every batch is sampled and decoded exactly once inside the timed region (no
+    work moves out of it); only the order of independent batches overlaps.
+    Measured (tools/dev/cu_split_probe.py, one box): sampling 1.03 s + decode
+    1.35 s in sequence = 2.38 s per batch; side by side on 128 + 128 CUs 2.17 s."""
+
+    def __init__(self, o, dev, start, count, sizes, world, gather):
+        from confild_amd.streams import CuRangeStream, cu_count
+        n = cu_count(dev)
+        h = int(os.environ.get("CFD_PIPE_SAMPLE_CUS", n // 2))   # CUs of the sampling half (development)
+        self.su = CuRangeStream(dev, 0, h)
+        self.sd = CuRangeStream(dev, h, n - h)
+        self.cus = (h, n - h)
+        self.cu_share = (n - h) / n
+        self.o, self.dev, self.start, self.count = o, dev, start, count
+        self.sizes, self.world, self.gather = sizes, world, gather
+
+    def _decode(self, den, ready, evd, stream=None):
+        # nothing is enqueued on the default stream between the first sample and the
+        # end: it is the legacy NULL stream, and any operation on it orders every
+        # blocking stream behind it (a wait there serialised the two halves)
+        sd = self.sd.stream if stream is None else stream
+        sd.wait_event(ready)
+        with torch.cuda.stream(sd):
+            d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            d0.record()
+            f = self.o["nf"].decode(self.o["coords"], den.reshape(self.count * S, 1, S), self.o["xn"], self.o["yn"])
+            d1.record()
+            f = gather_to_root(f, 0, self.sizes, self.world) if self.gather else f   # RCCL on this stream
+        den.record_stream(sd)
+        evd.append((d0, d1))
+        return f
+
+    def run(self, seeds):
+        """Samples and decodes one batch per seed; returns (sampling events,
+        the side-by-side decodes' events, the last batch's fields)."""
+        main = torch.cuda.current_stream(self.dev)
+        evu, evd, pend, out = [], [], None, None
+        for i, seed in enumerate(seeds):
+            if pend is not None:
+                out = self._decode(pend[0], pend[1], evd)
+                self.su.stream.wait_event(pend[1])   # the sampler's buffers: one batch at a time
+            with torch.cuda.stream(main if i == 0 else self.su.stream):
+                u0, u1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                u0.record()
+                den = sample_B(self.o, self.dev, seed, self.start, self.count)
+                u1.record()
+            evu.append((u0, u1))
+            pend = (den, u1)
+        # the last batch: its decode on the whole chip once both halves are done
+        main.wait_stream(self.su.stream)
+        main.wait_stream(self.sd.stream)
+        evl = []
+        out = self._decode(pend[0], pend[1], evl, stream=main)
+        return evu, evd, out
+
+    def close(self):
+        self.su.close()
+        self.sd.close()
+
+
 def step_B(o, dev, seed, start, count, ev=None):
     """This rank's samples [start, start+count) of one batch: sample -> de-normalise
     -> decode.  Returns fields (count*T, N, c).  ev: 3 events (U-Net start,
@@ -698,6 +772,9 @@ def main():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-gather", action="store_true", help="keep decoded fields on their ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="B: sample and decode each batch in sequence on the whole chip (the default pipelines "
+                         "from 4 timed steps)")
     ap.add_argument("--siren-compute", choices=["split_f16", "f32"], default="split_f16")
     ap.add_argument("--unet-compute", choices=["split_f16", "fp32"], default="split_f16")
     ap.add_argument("--per-gpu-batch", type=int, default=0,
@@ -784,17 +861,33 @@ def main():
     mode = nf.compute_mode(dev)
     kname, peak, peak_basis, _ = ROOFLINE[mode]
 
-    for w in range(args.warmup):
-        one(-1 - w)
-    barrier(dev, world)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        out = one(k, evs[k])
-    barrier(dev, world)
-    elapsed = max_over_ranks(time.perf_counter() - t0, dev, world)
-    unet_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in evs]))
-    dec_ms = float(np.mean([ev[1].elapsed_time(ev[2]) for ev in evs]))
+    # config B with >= 4 timed steps: the two-stage pipeline (PipelineB); the
+    # decoder's roofline is then against the MFMA peak of its CU half
+    pipe = PipelineB(o, dev, start, count, sizes, world, gather) if (
+        args.config == "B" and not args.no_pipeline and args.steps >= 4) else None
+    if pipe is not None:
+        if args.warmup:
+            pipe.run([10 ** 6 - 1 - w for w in range(args.warmup)])
+        barrier(dev, world)
+        t0 = time.perf_counter()
+        evu, evd, out = pipe.run([10 ** 6 + k for k in range(args.steps)])
+        barrier(dev, world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, dev, world)
+        unet_ms = float(np.mean([a.elapsed_time(b) for a, b in evu]))
+        dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evd]))   # the side-by-side decodes (half chip)
+        peak, peak_basis = peak * pipe.cu_share, f"{peak_basis} x the decode stream's CU share {pipe.cu_share:g}"
+    else:
+        for w in range(args.warmup):
+            one(-1 - w)
+        barrier(dev, world)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            out = one(k, evs[k])
+        barrier(dev, world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, dev, world)
+        unet_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in evs]))
+        dec_ms = float(np.mean([ev[1].elapsed_time(ev[2]) for ev in evs]))
     value = fields_per_step * args.steps / elapsed
     flops = rows_local * npts * siren_flops_per_pair(**c)
     achieved = flops / (dec_ms / 1e3) / 1e12
@@ -815,6 +908,7 @@ def main():
         else:
             workload = (f"config C (Case4 CNF-only): SIREN(3,384,3,15,384) decode of {C_LATENTS} latents x 2^22 "
                         f"uniform coords, coordinate-sharded")
+        dshare = 1.0 if pipe is None else pipe.cu_share
         rec = {
             "metric": METRIC if args.config == "B" else
             "decoded fields/sec (CNF-only, 2^22 coords per field), Case4 CNF, 1/2/4/8 GPU",
@@ -836,27 +930,38 @@ def main():
                          "peak": peak, "peak_basis": peak_basis, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": measured_traffic(mode, rows_local, npts) if args.config == "B" else None,
                          "flops_per_launch": flops, "launch_ms": dec_ms, "pmc": measured_mfma_util(kname),
-                         **({"peak_sustained": F16_SUSTAINED_TFLOPS / 3,
-                             "frac_sustained": achieved / (F16_SUSTAINED_TFLOPS / 3),
+                         **({"peak_sustained": F16_SUSTAINED_TFLOPS / 3 * dshare,
+                             "frac_sustained": achieved / (F16_SUSTAINED_TFLOPS / 3 * dshare),
                              "sustained_basis": "measured back-to-back f16 MFMA on random operands / 3 "
                                                 "(tools/mfma_chain.cpp, profiles/r02_mfma_chain.json)"}
                             if mode == "split_f16" else {})},
             "cpu_baseline": cpu,
             "rccl_ranks": world,
         }
+        if pipe is not None:
+            rec["pipeline"] = {"sample_cus": pipe.cus[0], "decode_cus": pipe.cus[1],
+                               "sample_ms_per_batch": unet_ms, "decode_ms_per_batch": dec_ms,
+                               "note": "batch k-1 decoded on one CU half while batch k samples on the other; "
+                                       "the first batch samples and the last decodes on the whole chip "
+                                       "(bench.py PipelineB); roofline.launch_ms = the side-by-side decodes"}
         if strong is not None:
             rec["strong"] = strong
         if args.config == "B":
             uf = count * UNET_FLOPS_PER_SAMPLE * 256
             ua = uf / (unet_ms / 1e3) / 1e12
+            # pipelined: all but the first batch sample on the other CU half
+            ush = 1.0 if pipe is None else (1 + (args.steps - 1) * pipe.cus[0] / sum(pipe.cus)) / args.steps
             rec["roofline_unet"] = {"bound": "mfma", "kernel": "U-Net forward x 256 steps (all kernels + step)",
-                                    "achieved": ua, "peak": F16_PEAK_TFLOPS / 3,
-                                    "peak_basis": "f16 dense MFMA peak / 3 (split-f16 convolutions)",
-                                    "unit": "TFLOP/s", "frac": ua / (F16_PEAK_TFLOPS / 3), "flops": uf,
+                                    "achieved": ua, "peak": F16_PEAK_TFLOPS / 3 * ush,
+                                    "peak_basis": "f16 dense MFMA peak / 3 (split-f16 convolutions)" +
+                                    ("" if pipe is None else f" x the sampling stream's mean CU share {ush:.3f}"),
+                                    "unit": "TFLOP/s", "frac": ua / (F16_PEAK_TFLOPS / 3 * ush), "flops": uf,
                                     "ms": unet_ms, "ms_per_forward": unet_ms / 256,
-                                    "peak_sustained": F16_SUSTAINED_TFLOPS / 3,
-                                    "frac_sustained": ua / (F16_SUSTAINED_TFLOPS / 3)}
+                                    "peak_sustained": F16_SUSTAINED_TFLOPS / 3 * ush,
+                                    "frac_sustained": ua / (F16_SUSTAINED_TFLOPS / 3 * ush)}
         print(json.dumps(rec), flush=True)
+    if pipe is not None:
+        pipe.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -53,6 +53,9 @@ _SIGS = {
     "cfd_unet_load_flat": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "cfd_unet_set_compute": (C.c_int, [C.c_void_p, C.c_int]),
     "cfd_unet_set_plan_batch": (C.c_int, [C.c_void_p, C.c_int]),
+    "cfd_device_cu_count": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
+    "cfd_stream_create_cu_range": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "cfd_stream_destroy": (C.c_int, [C.c_void_p]),
     "cfd_unet_check_finite": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_void_p]),
     "cfd_unet_workspace_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]),
     "cfd_unet_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,

@@ -17,6 +17,8 @@
 
 #include "sampler.hpp"
 
+#include <hip/hip_ext.h>
+
 struct cfd_sampler {
     const cfd_unet* unet = nullptr;
     const cfd_sched* sched = nullptr;
@@ -175,5 +177,35 @@ extern "C" int cfd_sampler_run(cfd_sampler* sp, const float* x_in, float* x_out,
             for (; k < k1; ++k) enqueue_step(sp, st);
         }
         if (x_out) CFD_HIP(hipMemcpyAsync(x_out, sp->x, bytes, hipMemcpyDeviceToDevice, st));
+    });
+}
+
+extern "C" int cfd_device_cu_count(int device, int* n_cu) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(n_cu, CFD_EARG, "null argument");
+        hipDeviceProp_t p;
+        CFD_HIP(hipGetDeviceProperties(&p, device));
+        *n_cu = p.multiProcessorCount;
+    });
+}
+
+extern "C" int cfd_stream_create_cu_range(int device, int first_cu, int n_cu, void** stream) {
+    return cfd::guard([&] {
+        CFD_REQUIRE(stream, CFD_EARG, "null argument");
+        int total = 0;
+        CFD_REQUIRE(cfd_device_cu_count(device, &total) == 0, CFD_EARG, "bad device");
+        CFD_REQUIRE(first_cu >= 0 && n_cu > 0 && first_cu + n_cu <= total, CFD_EARG, "CU range outside the device");
+        std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
+        for (int c = first_cu; c < first_cu + n_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+        cfd::DeviceGuard dg(device);
+        hipStream_t s = nullptr;
+        CFD_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+        *stream = (void*)s;
+    });
+}
+
+extern "C" int cfd_stream_destroy(void* stream) {
+    return cfd::guard([&] {
+        if (stream) CFD_HIP(hipStreamDestroy((hipStream_t)stream));
     });
 }

@@ -185,6 +185,13 @@ int  cfd_sampler_create(const cfd_unet* unet, const cfd_sched* sched, int kind, 
                         int64_t n_per_sample, int n_steps, const int64_t* host_tidx, const int64_t* host_tmodel,
                         int graph, int unroll, cfd_sampler** out);
 void cfd_sampler_destroy(cfd_sampler* sp);
+/* A stream whose kernels run on CUs [first_cu, first_cu + n_cu) of the device only
+ * (hipExtStreamCreateWithCUMask): the sampling loop and the CNF decode of the
+ * previous batch run side by side on disjoint halves of the chip (bench.py config
+ * B).  No reference counterpart (an execution resource). */
+int  cfd_device_cu_count(int device, int* n_cu);
+int  cfd_stream_create_cu_range(int device, int first_cu, int n_cu, void** stream);
+int  cfd_stream_destroy(void* stream);
 int  cfd_sampler_run(cfd_sampler* sp, const float* x_in, float* x_out, int k0, int k1, uint64_t seed,
                      uint64_t offset, void* stream);
 /* n standard normals from Philox4x32-10 (seed, counter) at stream positions

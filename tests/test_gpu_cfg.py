@@ -274,8 +274,9 @@ def test_configD_dps_chain_vs_oracle(hip):
     loop), each from the HIP path's own previous image, against the CPU oracle's
     autograd chain from the same start and noise (oracle/dps.py, itself pinned to
     the reference's steps at these widths by test_oracle_configD_dps_steps).  Per
-    step image <= 1e-4 of the latent scale and residual norm <= 1e-4 relative; the
-    chain's drift stays at that level (no chaotic growth)."""
+    step image <= 2e-5 of the latent scale and residual norm <= 1e-5 relative
+    [MI355X, round 5: the image error grows ~linearly, 7.9e-7 -> 4.5e-6 over the 12
+    steps; norms <= 9.4e-7]."""
     from confild_amd.guided.unet import create_model as guided_model
     from oracle import diffusion as od
     from oracle import dps as odps
@@ -309,8 +310,8 @@ def test_configD_dps_chain_vs_oracle(hip):
         en = abs(float(out["distance"][0]) - float(norm_ref)) / float(norm_ref)
         worst = max(worst, err)
         print(f"config D chain step {idx}: image {err:.2e}, norm rel {en:.2e}")
-        assert err <= 1e-4 and en <= 1e-4, (idx, err, en)
-    assert worst <= 1e-4
+        assert err <= 2e-5 and en <= 1e-5, (idx, err, en)
+    assert worst <= 2e-5
 
 
 def _case4_operator(tmp):
