@@ -810,6 +810,9 @@ def main():
         glob = sum(cnt for _, cnt in shards)
         start, count = shards[rank]
         sizes = [cnt * S for _, cnt in shards]
+        if args.plan_batch < 0 and count < B:
+            # fewer samples per GPU than 8 (--per-gpu-batch): plan the convolutions for them
+            o["model"].set_plan_batch(count)
 
         def one(k, ev=None):
             f = step_B(o, dev, seed=10 ** 6 + k, start=start, count=count, ev=ev)
@@ -817,24 +820,43 @@ def main():
 
         def strong_point():
             """Config B's global batch of 8 split over the ranks (the strong-scaling
-            point), timed like the main line, for the nested "strong" object."""
+            point), timed like the main line, for the nested "strong" object: the
+            model planned for the per-GPU share (so its sums differ in rounding from
+            the 8-per-GPU plan) and pipelined like the main line."""
             sh = b_shards("strong", world)
             st_, cn = sh[rank]
             sz = [c_ * S for _, c_ in sh]
-
-            def f(k):
-                r = step_B(o, dev, seed=2 * 10 ** 6 + k, start=st_, count=cn)
-                return gather_to_root(r, 0, sz, world) if gather else r
-            for w in range(args.warmup):
-                f(-1 - w)
-            barrier(dev, world)
-            t0 = time.perf_counter()
-            for k in range(args.steps):
-                f(k)
-            barrier(dev, world)
-            el = max_over_ranks(time.perf_counter() - t0, dev, world)
-            return {"value": B * args.steps / el, "unit": "fields/s", "ms_per_step": el / args.steps * 1e3,
-                    "global_batch": B, "per_gpu": [c_ for _, c_ in sh], "scaling": "strong"}
+            prev = o["model"].plan_batch
+            if args.plan_batch < 0:
+                o["model"].set_plan_batch(cn if cn < B else 0)
+            piped = not args.no_pipeline and args.steps >= 4
+            if piped:
+                pp = PipelineB(o, dev, st_, cn, sz, world, gather)
+                if args.warmup:
+                    pp.run([2 * 10 ** 6 - 1 - w for w in range(args.warmup)])
+                barrier(dev, world)
+                t0 = time.perf_counter()
+                pp.run([2 * 10 ** 6 + k for k in range(args.steps)])
+                barrier(dev, world)
+                el = max_over_ranks(time.perf_counter() - t0, dev, world)
+                pp.close()
+            else:
+                def f(k):
+                    r = step_B(o, dev, seed=2 * 10 ** 6 + k, start=st_, count=cn)
+                    return gather_to_root(r, 0, sz, world) if gather else r
+                for w in range(args.warmup):
+                    f(-1 - w)
+                barrier(dev, world)
+                t0 = time.perf_counter()
+                for k in range(args.steps):
+                    f(k)
+                barrier(dev, world)
+                el = max_over_ranks(time.perf_counter() - t0, dev, world)
+            res = {"value": B * args.steps / el, "unit": "fields/s", "ms_per_step": el / args.steps * 1e3,
+                   "global_batch": B, "per_gpu": [c_ for _, c_ in sh], "scaling": "strong",
+                   "plan_batch": o["model"].plan_batch or B, "pipelined": piped}
+            o["model"].set_plan_batch(prev)
+            return res
         c = CNF_B
         npts = GRID ** 3
         rows_local = count * S
@@ -938,6 +960,8 @@ def main():
             "cpu_baseline": cpu,
             "rccl_ranks": world,
         }
+        if args.config == "B":
+            rec["plan_batch"] = o["model"].plan_batch or B
         if pipe is not None:
             rec["pipeline"] = {"sample_cus": pipe.cus[0], "decode_cus": pipe.cus[1],
                                "sample_ms_per_batch": unet_ms, "decode_ms_per_batch": dec_ms,
