@@ -20,7 +20,7 @@ for d in sys.argv[1:]:
         for x in csv.DictReader(open(f)):
             kn = x["Kernel_Name"].replace("void ", "").replace("cfd::", "")
             kn = kn[:kn.find("(")] if "(" in kn else kn
-            if not any(p in kn for p in ("conv", "gn_", "attention", "attn", "splitk", "linear")):
+            if not any(p in kn for p in ("conv", "gn_", "gn2_", "attention", "attn", "splitk", "linear")):
                 continue
             key = kn[:44]
             acc[key][x["Counter_Name"]] += float(x["Counter_Value"])
