@@ -2292,7 +2292,8 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     CFD_REQUIRE(!a.src_bf16 || p.kx == 22, CFD_ESTATE, "internal: a bf16 convolution source needs the K1hb kernel");
     // K1s register-ring depth (development: CFD_CONV_PF; the tiles and their order,
     // hence the sums, do not depend on it)
-    static const int pf = env_int("CFD_CONV_PF", 1);
+    // (round 5 default 2: B = 8 64^2 3.95 -> 3.92 ms per step, others flat, r05as)
+    static const int pf = env_int("CFD_CONV_PF", 2);
     if (p.kx < 0) p.pf = pf >= 1 && pf <= 3 ? pf : 1;
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
     CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot + a.XC1 + a.XC2, CFD_ESHAPE, "conv K mismatch");
@@ -2301,7 +2302,7 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     CFD_REQUIRE(!a.tmode || ((a.stride == 1 || a.stride == 2) && !a.up), CFD_ESHAPE, "transposed conv: stride 1|2");
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
     CFD_REQUIRE(!(a.tmode && a.wbf && !a.wlo), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
-    static const int xcd = env_int("CFD_CONV_XCD", 3);   // round 5: 3 (PMC: 16^2 K1h L2 hit 0.19-0.27 -> 0.69-0.79)
+    static const int xcd = env_int("CFD_CONV_XCD", 4);   // round 5: 3 (PMC: 16^2 K1h L2 hit 0.19-0.27 -> 0.69-0.79), then 4
     static const int korder = env_int("CFD_CONV_KORDER", 0);
     static const int bufaddr = env_int("CFD_CONV_BUFADDR", 1);
     static const int ldsepi = env_int("CFD_CONV_LDSEPI", 1);
@@ -2311,8 +2312,11 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     // float4 rows need Cout % 4 == 0 and 16-B aligned bias / emb / res / out rows
     b.ldsepi = ldsepi && a.Cout % 4 == 0 && a.emb_stride % 4 == 0;
     // 1: splits-fastest XCD order; 2: m-fastest (weight-sharing) order; 3: order 2 where
-    // the per-sample image has <= 256 pixels (the small-M levels), else 1
-    b.xcd = xcd == 3 ? ((int64_t)a.Hout * a.Wout <= 256 ? 2 : 1) : xcd < 0 || xcd > 2 ? 1 : xcd;
+    // the per-sample image has <= 256 pixels (the small-M levels), else 1; 4: order 1
+    // for the bf16-operand convolutions (config E 4.66 -> 4.62 ms per step; the
+    // split-f16 config A is 0.3 % slower with it, r05as), 3 for the others
+    const int xo = xcd == 4 ? (a.wbf && !a.wlo ? 1 : 3) : xcd;
+    b.xcd = xo == 3 ? ((int64_t)a.Hout * a.Wout <= 256 ? 2 : 1) : xo < 0 || xo > 2 ? 1 : xo;
     b.korder = korder ? 1 : 0;
     {   // 32-bit buffer offsets and 24-bit pixel indices must hold
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));

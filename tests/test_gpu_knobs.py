@@ -1,6 +1,7 @@
 """Launch-shape switches that must not change a single bit: they pick how the
 work is scheduled -- the register-ring depth of the K1s convolution tiles
-(CFD_CONV_PF), the 64-channel small-batch workgroups of K1h / K1s (default,
+(CFD_CONV_PF, default 2), the convolution tiles' workgroup order over the XCDs
+(CFD_CONV_XCD: 3 the round-5 per-level order, 0 dispatch order; default 4), the 64-channel small-batch workgroups of K1h / K1s (default,
 CFD_CONV_SMALLN=0 restores 128), the K1h / K1hb split-K 2 run as two
 in-workgroup K groups instead of two workgroups and a partial slab
 (CFD_CONV_KHG: 1 wherever it applies; default 0, never), the K1hb register
@@ -59,8 +60,9 @@ def _run(env_extra):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("knob", ["CFD_CONV_PF=2", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0", "CFD_CONV_KHG=1",
-                                  "CFD_CONV_KHB_OCC=1", "CFD_CONV_LDSEPI=0", "CFD_ATTN_XCD=0"])
+@pytest.mark.parametrize("knob", ["CFD_CONV_PF=1", "CFD_CONV_PF=3", "CFD_CONV_SMALLN=0", "CFD_CONV_KHG=1",
+                                  "CFD_CONV_KHB_OCC=1", "CFD_CONV_LDSEPI=0", "CFD_ATTN_XCD=0", "CFD_CONV_XCD=3",
+                                  "CFD_CONV_XCD=0"])
 def test_schedule_switch_is_bit_identical(hip, knob):
     # K1h's in-workgroup K groups take no fused skip convolution (conv_takes_skip):
     # that switch is compared with the skip convolutions unfused on both sides
