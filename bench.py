@@ -194,7 +194,11 @@ def max_over_ranks(v, dev, world):
 
 
 def gather_to_root(x, dim, sizes, world):
-    if world == 1:
+    """Rank 0 receives every rank's slab concatenated along `dim` (RCCL gather).
+    A one-rank job without a process group returns x; with one (the world-size-1
+    RCCL test of the pipelined path) the collective runs."""
+    import torch.distributed as tdist
+    if world == 1 and not (tdist.is_available() and tdist.is_initialized()):
         return x
     from confild_amd import dist as cdist
     return cdist.gather_cat(x, dim, sizes, dst=0)
@@ -223,8 +227,12 @@ def setup_B(dev, rank, world, siren_compute, unet_compute, plan_batch=0):
     cdist.broadcast_module(model)
     cdist.broadcast_module(nf)
     model.set_compute(unet_compute)
-    # the default planned batch (8): the weak-scaling batch per GPU, and the same
-    # plan for the strong-scaling shards, so a sample's bits never depend on N
+    # the planned batch (cfd_unet_set_plan_batch): 0 = 8, config B's batch per GPU.
+    # main() re-plans for the per-GPU sample count when that is below 8 (the same
+    # count on every rank, so all ranks tile alike); the strong-scaling point plans
+    # for its largest shard -- a stated choice: its samples then differ from the
+    # 8-per-GPU plan's by fp32 rounding only (pinned over the whole 256-step loop by
+    # tests/test_gpu_cfg.py::test_configB_full_256_step_trajectory[plan1])
     model.set_plan_batch(max(plan_batch, 0))
     nf.set_compute(siren_compute)
     diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=STEPS)
@@ -286,14 +294,17 @@ class PipelineB:
         evd.append((d0, d1))
         return f
 
-    def run(self, seeds):
+    def run(self, seeds, keep=None):
         """Samples and decodes one batch per seed; returns (sampling events,
-        the side-by-side decodes' events, the last batch's fields)."""
+        the side-by-side decodes' events, the last batch's fields).  `keep` (a
+        list, tests): every batch's fields are appended to it in seed order."""
         main = torch.cuda.current_stream(self.dev)
         evu, evd, pend, out = [], [], None, None
         for i, seed in enumerate(seeds):
             if pend is not None:
                 out = self._decode(pend[0], pend[1], evd)
+                if keep is not None:
+                    keep.append(out)
                 self.su.stream.wait_event(pend[1])   # the sampler's buffers: one batch at a time
             with torch.cuda.stream(main if i == 0 else self.su.stream):
                 u0, u1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -307,11 +318,20 @@ class PipelineB:
         main.wait_stream(self.sd.stream)
         evl = []
         out = self._decode(pend[0], pend[1], evl, stream=main)
+        if keep is not None:
+            keep.append(out)
         return evu, evd, out
 
     def close(self):
         self.su.close()
         self.sd.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
 
 def step_B(o, dev, seed, start, count, ev=None):
@@ -810,9 +830,11 @@ def main():
         glob = sum(cnt for _, cnt in shards)
         start, count = shards[rank]
         sizes = [cnt * S for _, cnt in shards]
-        if args.plan_batch < 0 and count < B:
-            # fewer samples per GPU than 8 (--per-gpu-batch): plan the convolutions for them
-            o["model"].set_plan_batch(count)
+        big = max(cnt for _, cnt in shards)
+        if args.plan_batch < 0 and big < B:
+            # fewer samples per GPU than 8 (--per-gpu-batch): every rank plans the
+            # convolutions for the largest shard (one plan for the whole job)
+            o["model"].set_plan_batch(big)
 
         def one(k, ev=None):
             f = step_B(o, dev, seed=10 ** 6 + k, start=start, count=count, ev=ev)
@@ -826,37 +848,41 @@ def main():
             sh = b_shards("strong", world)
             st_, cn = sh[rank]
             sz = [c_ * S for _, c_ in sh]
+            big_s = max(c_ for _, c_ in sh)
             prev = o["model"].plan_batch
-            if args.plan_batch < 0:
-                o["model"].set_plan_batch(cn if cn < B else 0)
-            piped = not args.no_pipeline and args.steps >= 4
-            if piped:
-                pp = PipelineB(o, dev, st_, cn, sz, world, gather)
-                if args.warmup:
-                    pp.run([2 * 10 ** 6 - 1 - w for w in range(args.warmup)])
-                barrier(dev, world)
-                t0 = time.perf_counter()
-                pp.run([2 * 10 ** 6 + k for k in range(args.steps)])
-                barrier(dev, world)
-                el = max_over_ranks(time.perf_counter() - t0, dev, world)
-                pp.close()
-            else:
-                def f(k):
-                    r = step_B(o, dev, seed=2 * 10 ** 6 + k, start=st_, count=cn)
-                    return gather_to_root(r, 0, sz, world) if gather else r
-                for w in range(args.warmup):
-                    f(-1 - w)
-                barrier(dev, world)
-                t0 = time.perf_counter()
-                for k in range(args.steps):
-                    f(k)
-                barrier(dev, world)
-                el = max_over_ranks(time.perf_counter() - t0, dev, world)
-            res = {"value": B * args.steps / el, "unit": "fields/s", "ms_per_step": el / args.steps * 1e3,
-                   "global_batch": B, "per_gpu": [c_ for _, c_ in sh], "scaling": "strong",
-                   "plan_batch": o["model"].plan_batch or B, "pipelined": piped}
-            o["model"].set_plan_batch(prev)
-            return res
+            try:
+                if args.plan_batch < 0:
+                    o["model"].set_plan_batch(big_s if big_s < B else 0)
+                piped = not args.no_pipeline and args.steps >= 4
+                if piped:
+                    with PipelineB(o, dev, st_, cn, sz, world, gather) as pp:
+                        if args.warmup:
+                            pp.run([2 * 10 ** 6 - 1 - w for w in range(args.warmup)])
+                        barrier(dev, world)
+                        t0 = time.perf_counter()
+                        pp.run([2 * 10 ** 6 + k for k in range(args.steps)])
+                        barrier(dev, world)
+                        el = max_over_ranks(time.perf_counter() - t0, dev, world)
+                else:
+                    def f(k):
+                        r = step_B(o, dev, seed=2 * 10 ** 6 + k, start=st_, count=cn)
+                        return gather_to_root(r, 0, sz, world) if gather else r
+                    for w in range(args.warmup):
+                        f(-1 - w)
+                    barrier(dev, world)
+                    t0 = time.perf_counter()
+                    for k in range(args.steps):
+                        f(k)
+                    barrier(dev, world)
+                    el = max_over_ranks(time.perf_counter() - t0, dev, world)
+                return {"value": B * args.steps / el, "unit": "fields/s", "ms_per_step": el / args.steps * 1e3,
+                        "global_batch": B, "per_gpu": [c_ for _, c_ in sh], "scaling": "strong",
+                        "plan_batch": o["model"].plan_batch or B,
+                        "plan_note": "planned for the largest shard (a stated choice, DESIGN.md section 7): "
+                                     "samples equal the 8-per-GPU plan's within fp32 rounding, not bit for bit",
+                        "pipelined": piped}
+            finally:
+                o["model"].set_plan_batch(prev)
         c = CNF_B
         npts = GRID ** 3
         rows_local = count * S

@@ -78,7 +78,12 @@ struct cfd_unet {
     int compute = CFD_COMPUTE_SPLIT_F16;
     int plan_b = 0;   // the batch the convolution planner tiles for (0: 8); cfd_unet_set_plan_batch
     int tape_mode = CFD_TAPE_INPUT_VJP;   // what the next forward_tape records
-    int tape_mode_rec = CFD_TAPE_INPUT_VJP;   // what the last forward_tape recorded (the replays' layout)
+    // every live tape's recording: its layout (mode), batch and planned batch, so a
+    // replay (input_vjp / param_grad) walks the layout of the forward that wrote
+    // THAT tape, whatever was recorded since on other tapes (host-side: no sync)
+    struct TapeRec { int mode, B, plan; uint64_t seq; };
+    std::map<const void*, TapeRec> tapes;
+    uint64_t tape_seq = 0;
     int* nonfinite = nullptr;  // range guard flag: set by the last convolution on a non-finite eps
     mutable std::map<int, size_t> ws_cache;  // workspace bytes per B (the dry walk is host work)
     uint64_t version = 0;   // bumped by every set_param / set_compute: launch arguments (weight
@@ -1788,6 +1793,24 @@ extern "C" int cfd_unet_tape_bytes(const cfd_unet* h, int B, size_t* bytes) {
     });
 }
 
+namespace {
+constexpr size_t kMaxTapes = 64;   // live tapes remembered per handle (oldest forgotten first)
+
+// the recording a replay of `tape` at batch B must follow; loud on a tape this
+// handle did not record, or one recorded at another batch or plan
+const cfd_unet::TapeRec& tape_rec(const cfd_unet* h, const void* tape, int B, size_t tape_bytes) {
+    auto it = h->tapes.find(tape);
+    CFD_REQUIRE(it != h->tapes.end(), CFD_ESTATE,
+                "tape was not recorded by cfd_unet_forward_tape on this handle (or was forgotten: at most 64 live "
+                "tapes per handle)");
+    CFD_REQUIRE(it->second.B == B, CFD_EARG, "B differs from the batch the tape was recorded at");
+    CFD_REQUIRE(it->second.plan == plan_batch(h), CFD_ESTATE,
+                "the planned batch changed since the tape was recorded (cfd_unet_set_plan_batch)");
+    CFD_REQUIRE(tape_bytes >= tape_bytes_mode(h, B, it->second.mode), CFD_EARG, "tape too small");
+    return it->second;
+}
+}  // namespace
+
 extern "C" int cfd_unet_set_tape_mode(cfd_unet* h, int mode) {
     return cfd::guard([&] {
         CFD_REQUIRE(h, CFD_EARG, "null handle");
@@ -1830,8 +1853,15 @@ extern "C" int cfd_unet_forward_tape(cfd_unet* h, const float* x, const int64_t*
         Workspace ws{align256(workspace), 0, false}, tws{align256(tape), 0, false};
         Tape tp{&tws, nullptr};
         tp.keep_gnout = h->tape_mode == CFD_TAPE_PARAM_GRAD;
-        h->tape_mode_rec = h->tape_mode;
+        h->tapes.erase(tape);   // a re-recording replaces the old layout before anything runs
         run(h, x, t, eps, B, ws, (hipStream_t)stream, &tp, true);
+        h->tapes[tape] = {h->tape_mode, B, plan_batch(h), ++h->tape_seq};
+        while (h->tapes.size() > kMaxTapes) {
+            auto old = h->tapes.begin();
+            for (auto i = h->tapes.begin(); i != h->tapes.end(); ++i)
+                if (i->second.seq < old->second.seq) old = i;
+            h->tapes.erase(old);
+        }
     });
 }
 
@@ -1844,13 +1874,13 @@ extern "C" int cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, i
         size_t need = 0;
         cfd_unet_vjp_workspace_bytes(h, B, &need);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        CFD_REQUIRE(tape_bytes >= tape_bytes_mode(h, B, h->tape_mode_rec), CFD_EARG, "tape too small");
+        const int mode = tape_rec(h, tape, B, tape_bytes).mode;
         // replay the forward walk (no launches) over the same tape layout to
         // recover where every saved activation lives
         Workspace fws{nullptr, 0, true}, tws{align256(const_cast<void*>(tape)), 0, false};
         std::vector<Rec> recs;
         Tape tp{&tws, &recs};
-        tp.keep_gnout = h->tape_mode_rec == CFD_TAPE_PARAM_GRAD;
+        tp.keep_gnout = mode == CFD_TAPE_PARAM_GRAD;
         run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
         Workspace ws{align256(workspace), 0, false};
         run_vjp(h, d_eps, d_x, B, recs, ws, (hipStream_t)stream);
@@ -1876,11 +1906,11 @@ extern "C" int cfd_unet_param_grad(cfd_unet* h, const float* x, const float* d_e
         size_t need = 0;
         cfd_unet_param_grad_workspace_bytes(h, B, &need);
         CFD_REQUIRE(ws_bytes >= need, CFD_EARG, "workspace too small");
-        CFD_REQUIRE(tape_bytes >= tape_bytes_mode(h, B, h->tape_mode_rec), CFD_EARG, "tape too small");
+        const int mode = tape_rec(h, tape, B, tape_bytes).mode;
         Workspace fws{nullptr, 0, true}, tws{align256(const_cast<void*>(tape)), 0, false};
         std::vector<Rec> recs;
         Tape tp{&tws, &recs};
-        tp.keep_gnout = h->tape_mode_rec == CFD_TAPE_PARAM_GRAD;
+        tp.keep_gnout = mode == CFD_TAPE_PARAM_GRAD;
         run(h, nullptr, nullptr, nullptr, B, fws, nullptr, &tp, false);
         ParamGrad pg;
         pg.grad = grad;

@@ -161,8 +161,13 @@ class SIRENAutodecoder_film(nn.Module):
         if hit is not None and hit[0] is t and hit[1] == t._version:
             return hit[2]
         v = t.to(device=dev, dtype=torch.float32)
+        cache.pop(key, None)
         cache[key] = (t, t._version, v)
+        while len(cache) > self._NORM_CACHE_MAX:   # bounded: callers may build new normalisers per call
+            cache.pop(next(iter(cache)))
         return v
+
+    _NORM_CACHE_MAX = 8   # (max, min) of the coordinate and output normalisers, two devices
 
     def _norm_args(self, cf, N, dev, x_normalizer, y_normalizer):
         """Fusable '-11' normaliser bounds -> (coords, xmax, xmin, ymax, ymin, ystride, post)."""

@@ -20,11 +20,16 @@ def cu_count(device) -> int:
 
 
 class CuRangeStream:
-    """A torch-usable stream bound to CUs [first, first + count) of `device`."""
+    """A torch-usable stream bound to CUs [first, first + count) of `device`.
+
+    The HIP stream is destroyed by close() (also on leaving a ``with`` block, or
+    when the object is collected) after a device synchronise, so no queued work
+    and no caching-allocator block recorded on it outlives the stream."""
 
     def __init__(self, device, first: int, count: int):
         device = torch.device(device)
         self.device_index = device.index if device.index is not None else torch.cuda.current_device()
+        self._handle = None
         h = C.c_void_p()
         _lib.check(_lib.load().cfd_stream_create_cu_range(self.device_index, int(first), int(count), C.byref(h)),
                    "cfd_stream_create_cu_range")
@@ -37,3 +42,16 @@ class CuRangeStream:
             torch.cuda.synchronize(self.device_index)
             _lib.check(_lib.load().cfd_stream_destroy(self._handle), "cfd_stream_destroy")
         self._handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

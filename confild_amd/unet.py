@@ -294,9 +294,12 @@ class UNetModel(nn.Module):
         if not 0 <= int(nominal_batch) <= 64:
             raise ValueError("plan batch must be in 0..64")
         if int(nominal_batch) != self.plan_batch:
-            # the workspaces hold the split-K slab, sized per planned batch
+            # the workspaces hold the split-K slab, sized per planned batch; a tape
+            # recorded under the old plan cannot be replayed (the library refuses it)
             self._workspaces = {}
             self._vjp_ws, self._vjp_key = None, None
+            self._pg_ws, self._pg_key = None, None
+            self._taped = None
         self.plan_batch = int(nominal_batch)
         return self
 
@@ -546,7 +549,7 @@ class UNetModel(nn.Module):
 
     def _tape_buf(self, h, device, B):
         # sized for the mode of the last forward_tape (input_vjp / param_grad replay it)
-        key = (device, B, getattr(self, "_tape_mode", 0))
+        key = (device, B, getattr(self, "_tape_mode", 0), self.plan_batch)
         if getattr(self, "_tape_key", None) != key:
             n = C.c_size_t()
             _lib.check(_lib.load().cfd_unet_tape_bytes(h, B, C.byref(n)), "tape bytes")

@@ -134,7 +134,11 @@ int  cfd_unet_input_vjp(cfd_unet* h, const float* d_eps, float* d_x, int B, cons
  * the convolutions read and its max |.| -- the operands of cfd_unet_param_grad's
  * split weight gradients, which otherwise recompute them (one activation per
  * GroupNorm of tape memory, +0.3 ms per Case1 forward, -2.5 ms per backward).
- * input_vjp / param_grad replay the layout of the mode the tape was recorded in. */
+ * The handle remembers, per tape pointer, the mode, batch and planned batch each
+ * cfd_unet_forward_tape recorded (the 64 most recent tapes): input_vjp /
+ * param_grad replay THAT tape's layout, so several live tapes of different modes
+ * stay valid; replaying a tape the handle did not record (or recorded at another
+ * B or plan) fails with CFD_ESTATE / CFD_EARG instead of reading a wrong layout. */
 #define CFD_TAPE_INPUT_VJP  0
 #define CFD_TAPE_PARAM_GRAD 1
 int  cfd_unet_set_tape_mode(cfd_unet* h, int mode);

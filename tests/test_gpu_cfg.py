@@ -57,10 +57,16 @@ def _noise_list(tag, n, shape):
     return [torch.from_numpy(noise_for(tag, k, shape)).to(DEV) for k in range(n)]
 
 
-def test_configB_full_256_step_trajectory(hip):
+@pytest.mark.parametrize("plan", [0, 1, 2], ids=["plan8", "plan1", "plan2"])
+def test_configB_full_256_step_trajectory(hip, plan):
+    """The 256-step config-B loop against the reference, at the default planned
+    batch (8, the weak-scaling line) and at the plans the timed small-batch points
+    use (1: bench.py's strong-scaling shard at 8 GPUs and --per-gpu-batch 1;
+    2: its 4-GPU shard): the same 1e-5 bound at every plan."""
     c = TRAJ_B
     g = golden("golden_trajB.npz")
     m = _unet(c)
+    m.set_plan_batch(plan)
     d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=c["respacing"])
     assert np.array_equal(np.asarray(d.timestep_map), g["timestep_map"])
     shape = (c["B"], 1, c["image_size"], c["image_size"])
@@ -74,7 +80,7 @@ def test_configB_full_256_step_trajectory(hip):
             errs[k] = (_rel(out["sample"], g["samples"][j]), _rel(out["pred_xstart"], g["pred_xstart"][j]))
         final = out["sample"]
     errs["final"] = _rel(final, g["final"])
-    print("config-B trajectory drift (sample, x0) per checkpoint:", errs)
+    print(f"config-B trajectory drift at plan {plan or 8} (sample, x0) per checkpoint:", errs)
     assert errs["final"] <= 1e-5, errs
     assert max(v[0] for k, v in errs.items() if k != "final") <= 1e-5, errs
     assert max(v[1] for k, v in errs.items() if k != "final") <= 5e-4, errs
@@ -361,8 +367,11 @@ def test_case4_real_shape_dps_step(hip, tmp_path):
     os.remove(ema)
 
 
-def test_case4_real_shape_10_consecutive_dps_steps(hip, tmp_path):
-    """The notebook's loop body over 10 consecutive steps (indices 500..491) at
+@pytest.mark.parametrize("plan", [0, 2], ids=["plan8", "plan2"])
+def test_case4_real_shape_10_consecutive_dps_steps(hip, tmp_path, plan):
+    """Run at the default planned batch (8) and at the plan bench.py times real
+    Case4 with (DPS_CFG["Case4"]["plan_batch"] = 2: gn2's 1024-thread chunks at
+    384^2 and the plan-2 split-K counts).  The notebook's loop body over 10 consecutive steps (indices 500..491) at
     384^2, each step fed the previous step's output and the reference's noise:
     the drift of a chain, not one step.  Per step: image <= 5e-5 and x0_hat
     <= 3e-4 of max(1, |ref|) on the fixture's 4x-strided subgrid, residual norm
@@ -384,6 +393,7 @@ def test_case4_real_shape_10_consecutive_dps_steps(hip, tmp_path):
     ema = tmp_path / "ema_0.9999_400000.pt"
     torch.save({k: torch.from_numpy(v) for k, v in synth.unet_state_dict(c["unet_seed"], shapes).items()}, ema)
     model = guided_model(**kw, model_path=str(ema)).to(DEV)
+    model.set_plan_batch(plan)
     os.remove(ema)
     y = torch.from_numpy(golden("golden_case4op.npz")["A"]).to(DEV)
     cond, sampler = _guided("", op, 1.0)
@@ -405,7 +415,7 @@ def test_case4_real_shape_10_consecutive_dps_steps(hip, tmp_path):
     n_off = int((dfin > 5e-5).sum())
     print(f"Case4 final image: {n_off} of {dfin.size} elements beyond 5e-5, 99.9th percentile "
           f"{np.percentile(dfin, 99.9):.2e}")
-    print("Case4 384^2 10-step chain (idx, img, x0, norm, sum):", [tuple(round(v, 9) if isinstance(v, float) else v
+    print(f"Case4 384^2 10-step chain at plan {plan or 8} (idx, img, x0, norm, sum):", [tuple(round(v, 9) if isinstance(v, float) else v
                                                                      for v in e) for e in errs], f"final {e_fin:.2e}")
     assert max(e[1] for e in errs) <= 5e-5 and max(e[2] for e in errs) <= 3e-4, errs
     assert max(e[3] for e in errs) <= 1e-5 and max(e[4] for e in errs) <= 1e-5, errs

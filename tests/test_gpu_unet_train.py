@@ -354,3 +354,84 @@ def test_trainloop_ddp_two_ranks(hip, tmp_path):
     loop.forward_backward(torch.from_numpy(g["x0"]).to(DEV), noise=torch.from_numpy(g["noise"][0]).to(DEV))
     full = loop.grad.cpu()
     assert float((r0["grad"] - full).abs().max()) <= 2e-4 * float(full.abs().max())
+
+
+def test_tape_layout_is_per_tape_through_the_c_abi(hip):
+    """Two live tapes of different modes on one handle (C ABI directly): tape A
+    recorded for param_grad (CFD_TAPE_PARAM_GRAD), then tape B for the input-VJP
+    (the smaller layout).  param_grad on A afterwards replays A's own layout -- the
+    same gradients, bit for bit, as right after A was recorded -- and input_vjp on
+    B equals the Python API's.  A pointer the handle never recorded, and a replay
+    at another batch, are refused (no silent wrong layout)."""
+    import ctypes as C
+    from confild_amd import _lib
+    g, cfg, sd, m = _unet("wide128")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    t = torch.from_numpy(g["t"]).to(DEV)
+    d = torch.from_numpy(synth.normal(5, "tapes/d", tuple(x.shape))).to(DEV)
+    B = x.shape[0]
+    lib = _lib.load()
+    h = m._handle(DEV)
+    ws = m._workspace(h, DEV, B)
+    st = _lib.stream_of(DEV)
+    P = _lib.ptr
+
+    def nbytes(fn):
+        n = C.c_size_t()
+        _lib.check(fn(h, B, C.byref(n)), "bytes")
+        return n.value
+
+    def record(mode, xx):
+        _lib.check(lib.cfd_unet_set_tape_mode(h, mode), "mode")
+        tape = torch.empty(nbytes(lib.cfd_unet_tape_bytes), dtype=torch.uint8, device=DEV)
+        eps = torch.empty_like(xx)
+        _lib.check(lib.cfd_unet_forward_tape(h, P(xx), P(t), P(eps), B, P(ws), ws.numel(), P(tape), tape.numel(), st),
+                   "forward_tape")
+        return tape
+
+    pws = torch.empty(nbytes(lib.cfd_unet_param_grad_workspace_bytes), dtype=torch.uint8, device=DEV)
+    vws = torch.empty(nbytes(lib.cfd_unet_vjp_workspace_bytes), dtype=torch.uint8, device=DEV)
+    n_total = sum(p.numel() for p in m.parameters())
+
+    def pgrad(tape):
+        gr = torch.zeros(n_total, device=DEV)
+        _lib.check(lib.cfd_unet_param_grad(h, P(x), P(d), B, P(tape), tape.numel(), P(gr), P(pws), pws.numel(), st),
+                   "param_grad")
+        return gr
+
+    tape_a = record(1, x)
+    g_a = pgrad(tape_a)
+    x2 = (x * 0.5 + 0.1).contiguous()
+    tape_b = record(0, x2)
+    assert tape_b.numel() < tape_a.numel()
+    assert torch.equal(pgrad(tape_a), g_a)
+    dx = torch.empty_like(x)
+    _lib.check(lib.cfd_unet_input_vjp(h, P(d), P(dx), B, P(tape_b), tape_b.numel(), P(vws), vws.numel(), st), "vjp")
+    m.forward_tape(x2, t)
+    assert torch.equal(m.input_vjp(d), dx)
+    stray = torch.empty_like(tape_a)
+    with pytest.raises(_lib.CfdError, match="not recorded"):
+        _lib.check(lib.cfd_unet_input_vjp(h, P(d), P(dx), B, P(stray), stray.numel(), P(vws), vws.numel(), st), "vjp")
+    with pytest.raises(_lib.CfdError, match="batch"):
+        _lib.check(lib.cfd_unet_input_vjp(h, P(d), P(dx), 1, P(tape_b), tape_b.numel(), P(vws), vws.numel(), st),
+                   "vjp")
+
+
+def test_param_grad_after_plan_batch_change(hip):
+    """param_grad, then set_plan_batch(2), then forward_tape + param_grad: the
+    param-grad workspace (it holds the split-K slab, sized per planned batch) is
+    re-sized, and the gradients stay within fp32 rounding of the default plan's."""
+    g, cfg, sd, m = _unet("wide128")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    t = torch.from_numpy(g["t"]).to(DEV)
+    d = torch.from_numpy(synth.normal(5, "pgplan/d", tuple(x.shape))).to(DEV)
+    m.forward_tape(x, t)
+    ref = m.param_grad(d)
+    for pb in (2, 1):
+        m.set_plan_batch(pb)
+        with pytest.raises(RuntimeError):
+            m.param_grad(d)          # the tape of the old plan is not replayed
+        m.forward_tape(x, t)
+        got = m.param_grad(d)
+        err = float((got - ref).abs().max()) / float(ref.abs().max())
+        assert torch.isfinite(got).all() and err < 1e-4, (pb, err)
