@@ -1247,7 +1247,6 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_HIP(hipMalloc(&h->wimg32, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wimg32r, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wrev, sizeof(float) * 2 * (size_t)std::max(nh, 1)));
-        if (const char* e = getenv("CFD_SIREN_COMPUTE")) h->compute = atoi(e);
         *out = h;
     });
 }
@@ -1399,14 +1398,11 @@ extern "C" int cfd_siren_forward(cfd_siren* h, const float* coords, int64_t N, c
         a.d = h->cfg.in_coord_features;
         a.c = h->cfg.out_features;
         a.nh = nh;
+        a.stamps = cfd::stamps_buf();
         a.w0f = h->cfg.w0;
         if (h->compute == CFD_SIREN_SPLIT_F16 && nh >= 1 && cfd::siren_split_supported(h->NB)) {
             a.wscale = h->wscale;
-            static const bool use32 = [] {
-                const char* e = getenv("CFD_SIREN_SPLIT32");
-                return !e || atoi(e) != 0;
-            }();
-            if (use32 && cfd::siren_split32_supported(H, nh)) {
+            if (cfd::siren_split32_supported(H, nh)) {   // K7t; K7s for the other widths
                 a.wimg = h->wimg32;
                 a.wimg_rev = h->wimg32r;
                 a.wrev = h->wrev;
@@ -1492,10 +1488,8 @@ void launch_tape_ks(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
 template <int NB>
 void launch_tape_nb(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
     // K-split tiles where one wave per 16 pairs leaves most SIMDs idle
-    // (CFD_SIREN_TAPE_KS=0: the one-wave-per-tile kernels everywhere)
-    static const int ks_env = getenv("CFD_SIREN_TAPE_KS") ? atoi(getenv("CFD_SIREN_TAPE_KS")) : 1;
     if constexpr (NB % 4 == 0 && NB <= 24) {
-        if (ks_env && a.P < 16 * 2048) return launch_tape_ks<NB, 4>(a, bwd, st);
+        if (a.P < 16 * 2048) return launch_tape_ks<NB, 4>(a, bwd, st);
     }
     switch (tape_waves(a.P)) {
         case 4: return launch_tape_w<NB, 4>(a, bwd, st);

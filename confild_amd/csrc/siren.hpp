@@ -39,7 +39,10 @@ struct SirenArgs {
     int64_t b0;           // first latent of this launch (grid.y chunking)
     int d, c, nh;
     float w0f;
+    unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
 };
+// the CFD_STAMPS build's timestamp buffer (unet_kernels.hip; null: off)
+unsigned long long* stamps_buf();
 
 // LDS-DMA of one weight block (NB pieces of 1 KiB) into an LDS ring slot: one
 // global_load_lds_dwordx4 wave-instruction per piece, pieces spread over the waves.

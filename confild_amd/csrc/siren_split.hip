@@ -488,6 +488,14 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
     const int64_t b = p.b0 + blockIdx.y;
     const int64_t n = (int64_t)blockIdx.x * TILE + wave * 32 + (lane & 31);
     CFD_DASSERT(p.d >= 1 && p.d <= 4 && p.c >= 1 && p.c <= 4 && nh >= 1);
+#ifdef CFD_STAMPS
+    // the in-kernel clock (tools/dev/siren_clock.py): entry / exit stamps of
+    // s_memrealtime (100 MHz) and s_memtime (shader cycles) on every 61st tile
+    // column, spread over the XCDs (kind 5, launch field = the latent)
+    const bool stamped = blockIdx.x % 61 == 0;
+    if (stamped) CFD_STAMP(p.stamps, 5, (unsigned)blockIdx.y, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
 
     {
         const float* fsrc = p.film + b * (int64_t)(nh + 1) * H;
@@ -697,15 +705,12 @@ __global__ __launch_bounds__(256, 1) void siren_split32(SirenArgs p) {
             }
         }
     }
+#ifdef CFD_STAMPS
+    if (stamped) CFD_STAMP(p.stamps, 5, (unsigned)blockIdx.y, 4);
+#endif
 }
 
 namespace {
-
-int env_int(const char* name, int dflt, int lo, int hi) {
-    const char* e = getenv(name);
-    const int v = e ? atoi(e) : dflt;
-    return v >= lo && v <= hi ? v : dflt;
-}
 
 template <int NB, int RING, int CG, int RB = 1, bool NOSYNC = false, bool PKSIN = true>
 void launch_ring(SirenArgs a, int b, hipStream_t st) {
@@ -759,20 +764,19 @@ bool siren_split32_supported(int H, int nh) {
            sizeof(float) * ((size_t)4 * (H / 32) * 512 + film) <= 160 * 1024;
 }
 
-// HWSIN 4 (default): weights pre-scaled by w0/2pi, v_sin_f32 on the revolutions;
-// 3 (CFD_SIREN_HWSIN=3): the same after an explicit fract.  The radian-domain
-// sines (0: polynomial, 1: 2pi Cody-Waite, 2: reduction in revolutions) stay
-// in the sine probe (cfd_sine_probe) and the K7s/K9d kernels; their full
-// decoder instantiations and the timing experiments were removed in round 3.
+// HWSIN 4: weights pre-scaled by w0/2pi, v_sin_f32 on the revolutions (the
+// explicit-fract form, 3, measured the same and was removed in round 6).  The
+// radian-domain sines (0: polynomial, 1: 2pi Cody-Waite, 2: reduction in
+// revolutions) stay in the sine probe (cfd_sine_probe) and the K7s/K9d kernels;
+// their full decoder instantiations were removed in round 3.
 void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st) {
-    static const int hw = env_int("CFD_SIREN_HWSIN", 4, 3, 4);
     CFD_REQUIRE(a.wimg_rev && a.wrev, CFD_EARG, "split32 revolution image not set");
     a.wimg = a.wimg_rev;
     switch (H) {
-        case 64: return hw == 3 ? launch_split32<2, 0, 3>(a, b, st) : launch_split32<2, 0, 4>(a, b, st);
-        case 128: return hw == 3 ? launch_split32<4, 0, 3>(a, b, st) : launch_split32<4, 0, 4>(a, b, st);
-        case 256: return hw == 3 ? launch_split32<8, 0, 3>(a, b, st) : launch_split32<8, 0, 4>(a, b, st);
-        case 384: return hw == 3 ? launch_split32<12, 0, 3>(a, b, st) : launch_split32<12, 0, 4>(a, b, st);
+        case 64: return launch_split32<2, 0, 4>(a, b, st);
+        case 128: return launch_split32<4, 0, 4>(a, b, st);
+        case 256: return launch_split32<8, 0, 4>(a, b, st);
+        case 384: return launch_split32<12, 0, 4>(a, b, st);
         default: throw Error{CFD_EARG, "32x32 split-f16 SIREN needs hidden_features in {64, 128, 256, 384}"};
     }
 }

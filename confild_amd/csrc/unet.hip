@@ -272,8 +272,7 @@ uint16_t to_bf16(float f) {
 // split compute: f16 hi / lo parts and 1/s of an input-gradient pack into a
 // (nothing in the other modes: their transposed convolutions run in fp32)
 void PTS(const cfd_unet* h, const std::string& key, cfd::ConvArgs* a) {
-    static const bool on = !getenv("CFD_VJP_SPLIT") || atoi(getenv("CFD_VJP_SPLIT")) != 0;  // 0: fp32 (A/B)
-    if (h->compute != CFD_COMPUTE_SPLIT_F16 || !on) return;
+    if (h->compute != CFD_COMPUTE_SPLIT_F16) return;
     auto it = h->index.find(key);
     CFD_REQUIRE(it != h->index.end() && h->params[it->second].tpack, CFD_EKEY, "internal: missing conv " + key);
     const auto& p = h->params[it->second];
@@ -385,11 +384,8 @@ Sizes sizes(const cfd_unet* h) {
 // split-K partial slab
 constexpr size_t kSplitPer8 = size_t(16) << 20;
 // the batch the convolution planner and gn2 tile for: the model's setting
-// (cfd_unet_set_plan_batch), else CFD_PLAN_B (development), else 8
-int plan_batch(const cfd_unet* h) {
-    static const int env = getenv("CFD_PLAN_B") ? std::max(1, atoi(getenv("CFD_PLAN_B"))) : 8;
-    return h->plan_b > 0 ? h->plan_b : env;
-}
+// (cfd_unet_set_plan_batch), else 8
+int plan_batch(const cfd_unet* h) { return h->plan_b > 0 ? h->plan_b : 8; }
 // (kSplitPer8 per planned batch: plan_conv keeps splits * (plan_b samples' M x N)
 // within it, so ceil(B / plan_b) of those cover any real batch)
 size_t split_cap(const cfd_unet* h, int B) {
@@ -498,10 +494,9 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             *stats = g.stats = keep((size_t)B * 64);
         }
         g.out = nbuf;
-        // CFD_TAPE_PARAM_GRAD tapes keep it (CFD_TAPE_GNOUT=0 overrides: the weight
+        // CFD_TAPE_PARAM_GRAD tapes keep it (the input-VJP tapes do not: the weight
         // gradients then recompute the activated input)
-        static const int tape_gnout = getenv("CFD_TAPE_GNOUT") ? atoi(getenv("CFD_TAPE_GNOUT")) : 1;
-        if (tape && actp && tape_gnout && tape->keep_gnout) {   // kept for the weight gradients, with its range
+        if (tape && actp && tape->keep_gnout) {   // kept for the weight gradients, with its range
             CFD_REQUIRE(!bf16_out && ngs < kGnSlots, CFD_ESTATE, "internal: kept GroupNorm output");
             g.out = keep((size_t)B * in.H * in.W * in.C());
             g.amax_out = gslots + ngs++;
@@ -519,7 +514,6 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
             g.kpart = pend.a.part;
             g.ksplits = pend.splits;
             g.kbias = pend.a.bias;
-            g.kbias2 = pend.a.bias2;
             g.kemb = pend.a.emb;
             g.kemb_stride = pend.a.emb_stride;
             g.kres = pend.a.res;
@@ -579,51 +573,11 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
         const cfd::ConvArgs a = conv_args(n, pre, cout, 3, 1, 0, nullptr, nullptr, nullptr);
         return a.wbf && !a.wlo && cfd::conv_runs_k1hb(a, plan_checked(h, a, kSplitCap));
     };
-    // tweak: adjusts the launch arguments once the plan is known (the qkv K / V pack);
-    // a fused skip convolution (ConvArgs::xsrc1, fuse_skip) is planned as one GEMM
+    // tweak: adjusts the launch arguments once the plan is known (the qkv K / V pack)
     using Tweak = std::function<void(cfd::ConvArgs&, const cfd::ConvPlan&)>;
-    // A ResBlock's skip 1x1 convolution (unet.py:255-256) fused into its out_layers
-    // convolution as extra K over the raw block input x: out = [W_out | W_skip] x
-    // [h taps | x] + b_out + b_skip, one GEMM on K1h / K1x, no skip tensor.  The two
-    // weight packs keep their power-of-two scales; the operand of the smaller scale's
-    // side is staged times the ratio (<= 1, exact), acc_scale undoes the other.
-    // Returns false (args untouched) where the plan cannot take it: the skip runs as
-    // its own convolution then.  Off by default (CFD_CONV_SKIPFUSE=1: on, K1h only;
-    // 2: K1x too): measured 3.99 vs 3.97 ms per config-B B = 8 step, 3.07-3.09 vs
-    // 3.04-3.07 at B = 1 (graph loop, same box) -- the X steps, one 32-channel chunk
-    // each behind a two-step prefetch, cost what the separate launch did.
-    static const int skipfuse = getenv("CFD_CONV_SKIPFUSE") ? atoi(getenv("CFD_CONV_SKIPFUSE")) : 0;
-    auto fuse_skip = [&](const Act& hn, const Act& x, const std::string& pre, int cout, float* out,
-                         cfd::ConvArgs* fa) -> bool {
-        if (!skipfuse || h->compute != CFD_COMPUTE_SPLIT_F16) return false;
-        cfd::ConvArgs a = conv_args(hn, pre + ".out_layers.3", cout, 3, 1, 0, nullptr, nullptr, out);
-        float inv_x = 1.f;
-        a.xsrc1 = x.a;
-        a.xsrc2 = x.b;
-        a.XC1 = x.Ca;
-        a.XC2 = x.Cb;
-        a.xwbf = PB(h, pre + ".skip_connection.weight");
-        a.xwlo = PL(h, pre + ".skip_connection.weight", &inv_x);
-        a.bias2 = P(h, pre + ".skip_connection.bias");
-        const float inv_o = a.acc_scale;
-        if (inv_x >= inv_o) {
-            a.main_scale = inv_o / inv_x;
-            a.x_scale = 1.f;
-            a.acc_scale = inv_x;
-        } else {
-            a.main_scale = 1.f;
-            a.x_scale = inv_x / inv_o;
-            a.acc_scale = inv_o;
-        }
-        a.K += x.C();
-        if (!cfd::conv_takes_skip(a, plan_checked(h, a, kSplitCap))) return false;
-        *fa = a;
-        return true;
-    };
     auto conv = [&](const Act& in, const std::string& pre, int cout, int ks, int stride, int up,
-                    const float* embp, const float* resp, float* out, const Tweak& tweak = {},
-                    const cfd::ConvArgs* fused = nullptr) {
-        cfd::ConvArgs a = fused ? *fused : conv_args(in, pre, cout, ks, stride, up, embp, resp, out);
+                    const float* embp, const float* resp, float* out, const Tweak& tweak = {}) {
+        cfd::ConvArgs a = conv_args(in, pre, cout, ks, stride, up, embp, resp, out);
         flush();
         const cfd::ConvPlan plan = plan_checked(h, a, kSplitCap);
         if (tweak) tweak(a, plan);
@@ -631,9 +585,9 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     "internal: bf16 GroupNorm output feeds a convolution other than K1hb at " + pre);
         static const int conv_log = getenv("CFD_CONV_LOG") ? atoi(getenv("CFD_CONV_LOG")) : 0;
         if (conv_log && launch)   // development: one line per convolution, in launch order
-            fprintf(stderr, "CONV %s %dx%d C=%d+%d->%d ks=%d s=%d up=%d M=%d kx=%d bm=%d bn=%d nw=%d splits=%d xc=%d\n",
+            fprintf(stderr, "CONV %s %dx%d C=%d+%d->%d ks=%d s=%d up=%d M=%d kx=%d bm=%d bn=%d nw=%d splits=%d\n",
                     pre.c_str(), a.Hin, a.Win, a.C1, a.C2, a.Cout, a.ks, a.stride, a.up, a.M, plan.kx, plan.bm,
-                    plan.bn, plan.nw, plan.splits, a.XC1 + a.XC2);
+                    plan.bn, plan.nw, plan.splits);
         if (launch) {
             const int sp = cfd::launch_conv(a, plan, st, /*defer=*/true);   // the splits it left to reduce
             if (sp > 1) {
@@ -708,12 +662,12 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 // h = in_layers(x) + emb_layers(emb)   (unet.py:236-254)
                 const Act xin = gn(cur, r.pre + ".in_layers.0", 1, &rec.ss1, &rec.st1, true,
                                    feeds_k1hb(cur, r.pre + ".in_layers.2", r.cout), &rec.act1, &rec.amx1);
-                // skip(x) (unet.py:255-256): fused into the out_layers convolution
-                // below where the plan takes it, else its own convolution just before
-                // it (in_layers' deferred reduction still meets the out_layers GroupNorm)
+                // skip(x) (unet.py:255-256): its own convolution just before the
+                // out_layers one (in_layers' deferred reduction still meets the
+                // out_layers GroupNorm), read back as that convolution's residual
                 const float* resp = nullptr;
                 if (r.cin != r.cout) {
-                    resp = skipb;   // unless the out_layers convolution takes it (fuse_skip below)
+                    resp = skipb;
                 } else {
                     CFD_REQUIRE(cur.b == nullptr, CFD_ESTATE, "identity skip on a concatenated input");
                     resp = cur.a;
@@ -725,14 +679,9 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                 const Act hn = gn(th, r.pre + ".out_layers.0", 1, &rec.ss2, &rec.st2, /*keep_raw=*/tape != nullptr,
                                   feeds_k1hb(th, r.pre + ".out_layers.3", r.cout), &rec.act2, &rec.amx2);
                 float* out = dest(cur.a, cur.b, nout);
-                cfd::ConvArgs fa{};
-                if (r.cin != r.cout && fuse_skip(hn, cur, r.pre, r.cout, out, &fa)) {
-                    conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, nullptr, out, {}, &fa);
-                } else {
-                    if (r.cin != r.cout)   // reads the block input, still intact: out is another buffer
-                        conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
-                    conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
-                }
+                if (r.cin != r.cout)   // reads the block input, still intact: out is another buffer
+                    conv(cur, r.pre + ".skip_connection", r.cout, 1, 1, 0, nullptr, nullptr, skipb);
+                conv(hn, r.pre + ".out_layers.3", r.cout, 3, 1, 0, nullptr, resp, out);
                 cur = Act{out, r.cout, nullptr, 0, cur.H, cur.W};
                 break;
             }
@@ -1139,10 +1088,9 @@ void run_vjp(const cfd_unet* h, const float* d_eps, float* d_x, int B, const std
                 dconv(dout, at.C, in.H, in.W, at.pre + ".proj_out.weight", at.C, in.H, in.W, 1, 1, 0, 0, dA);
                 cfd::AttnBwdArgs ab{r.qkv, r.o, dA, r.lse, dd, dqkv, T, at.C,
                                     (float)(1.0 / std::sqrt(std::sqrt((double)at.ch)))};
-                // split compute: K9s (three f16 MFMAs per product); CFD_ATTN_BWD_SPLIT=0
-                // keeps the fp32-MFMA kernels (A/B)
-                static const int abs_on = getenv("CFD_ATTN_BWD_SPLIT") ? atoi(getenv("CFD_ATTN_BWD_SPLIT")) : 1;
-                if (abs_on && h->compute == CFD_COMPUTE_SPLIT_F16 && cfd::attention_bwd_split_ok(T, at.ch)) {
+                // split compute: K9s (three f16 MFMAs per product); the fp32 mode keeps
+                // the fp32-MFMA kernels
+                if (h->compute == CFD_COMPUTE_SPLIT_F16 && cfd::attention_bwd_split_ok(T, at.ch)) {
                     CFD_REQUIRE(cfd::attention_bwd_split_floats(T, at.C) <= z.max_abw, CFD_ESTATE,
                                 "internal: attention backward workspace");
                     cfd::launch_attention_bwd_split(ab, at.ch, at.heads, B, abws, st);
@@ -1226,7 +1174,6 @@ extern "C" int cfd_unet_create(const cfd_unet_cfg* cfg, int device, cfd_unet** o
             CFD_HIP(hipMalloc(&h->arena_lo, sizeof(uint16_t) * std::max<size_t>(h->arena_floats, 4)));
             CFD_HIP(hipMalloc(&h->arena_thi, sizeof(uint16_t) * std::max<size_t>(h->arena_t_floats, 4)));
             CFD_HIP(hipMalloc(&h->arena_tlo, sizeof(uint16_t) * std::max<size_t>(h->arena_t_floats, 4)));
-            if (const char* e = getenv("CFD_UNET_COMPUTE")) h->compute = atoi(e);
             const int half = cfg->model_channels / 2;
             // freqs = exp(-ln(10000) * arange(half, fp32) / half) in fp32 (nn.py:129-131)
             std::vector<float> fr(half);

@@ -194,97 +194,12 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GnArgs a) {
     if (a.amax_out) block_amax_atomic(mx, a.amax_out);
 }
 
-// K3f: the same GroupNorm(+SiLU) in ONE launch: workgroup = (sample, group).
-// Pass 1 sums the group's HW x cpg elements (thread t: channel quad t % nq of
-// every (256/nq)-th pixel, float64), a fixed-order tree gives mean / rstd; pass
-// 2 re-reads the same elements (L2-resident: the 32 groups of one sample run on
-// one XCD, see the block mapping) and writes y = x*scale + shift (+ SiLU).
-// Same statistics, affine form and output as the three-kernel path, one launch
-// instead of three (the path is latency-bound at these sizes); batch-invariant
-// (a sample's summation order does not depend on B).
-__global__ __launch_bounds__(256) void gn_fused_kernel(GnArgs a) {
-    // linear block L -> (b = L % B, grp = L / B): consecutive L go round-robin over
-    // the 8 XCDs, so with B % 8 == 0 every group of sample b shares one L2
-    const int L = blockIdx.x;
-    const int64_t b = L % a.B;
-    const int grp = L / a.B;
-    const int Ctot = a.Ctot, cpg = Ctot / 32, nq = cpg / 4;
-    const int HW = a.HW;
-    const int rows = 256 / nq;  // pixels per sweep
-    const int t = threadIdx.x;
-    const bool act = t < rows * nq;
-    const int q = t % nq, r0 = t / nq;
-    const int c = grp * cpg + 4 * q;
-    const float* src = c < a.C1 ? a.src1 + b * HW * a.C1 + c : a.src2 + b * HW * a.C2 + (c - a.C1);
-    const int ld = c < a.C1 ? a.C1 : a.C2;
-    __shared__ double red[2][256];
-    __shared__ float sh[2][32];
-    double s = 0, s2 = 0;
-    if (act) {
-        for (int p = r0; p < HW; p += rows) {
-            const f4 v = *(const f4*)(src + (int64_t)p * ld);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                s += v[j];
-                s2 += (double)v[j] * v[j];
-            }
-        }
-    }
-    red[0][t] = s;
-    red[1][t] = s2;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {  // fixed-order tree
-        if (t < w) {
-            red[0][t] += red[0][t + w];
-            red[1][t] += red[1][t + w];
-        }
-        __syncthreads();
-    }
-    if (t < cpg) {
-        const double n = (double)HW * cpg;
-        const double mean = red[0][0] / n;
-        const double var = fmax(red[1][0] / n - mean * mean, 0.0);
-        const float mf = (float)mean, rf = (float)(1.0 / sqrt(var + (double)a.eps));
-        const int cc = grp * cpg + t;
-        const float sc = rf * a.gamma[cc];
-        const float sf = a.beta[cc] - mf * sc;
-        sh[0][t] = sc;
-        sh[1][t] = sf;
-        a.ss[(b * Ctot + cc) * 2 + 0] = sc;
-        a.ss[(b * Ctot + cc) * 2 + 1] = sf;
-        if (a.stats && t == 0) {
-            a.stats[(b * 32 + grp) * 2 + 0] = mf;
-            a.stats[(b * 32 + grp) * 2 + 1] = rf;
-        }
-    }
-    __syncthreads();
-    float mx = 0.f;
-    if (act) {
-        f4 sc, sf;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            sc[j] = sh[0][4 * q + j];
-            sf[j] = sh[1][4 * q + j];
-        }
-        const int64_t dst = b * HW * Ctot + c;
-        for (int p = r0; p < HW; p += rows) {
-            f4 v = *(const f4*)(src + (int64_t)p * ld);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                v[j] = v[j] * sc[j] + sf[j];
-                if (a.silu) v[j] = silu_f(v[j]);
-            }
-            gn_store4(a, dst + (int64_t)p * Ctot, v);
-            mx = fmaxf(mx, amax4(v));
-        }
-    }
-    if (a.amax_out) block_amax_atomic(mx, a.amax_out);
-}
-
-// Register-resident form for HW x cpg <= 512 x IPT x 4: 512 threads, each
-// loading its IPT float4 at once (the loads pipeline instead of forming a
-// latency chain), summing them, and normalising the same registers (one HBM
-// read instead of two).  Same statistics / order semantics as gn_fused_kernel.
+// GroupNorm in one launch, one workgroup per (sample, group), for HW x cpg <=
+// NT x IPT x 4: every thread loads its IPT float4 at once (the loads pipeline
+// instead of forming a latency chain), a fixed-order float64 tree gives mean /
+// rstd, and the same registers are normalised (one HBM read): y = x*scale +
+// shift (+ SiLU).  Same statistics, affine form and output as the three-kernel
+// path; batch-invariant (a sample's summation order does not depend on B).
 template <int IPT, int NT = 512>
 __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     const int L = blockIdx.x;
@@ -317,11 +232,10 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
     if (ksrc) {  // constant false for IPT > 16: the branch folds away
         // split-K source (GnArgs::kpart): reduce, epilogue, store x, keep it
         const int64_t slab = (int64_t)a.B * HW * a.C1;
-        f4 kb = {0.f, 0.f, 0.f, 0.f}, kb2 = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
+        f4 kb = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (a.kbias) kb[j] = a.kbias[c + j];
-            if (a.kbias2) kb2[j] = a.kbias2[c + j];
             if (a.kemb) ke[j] = a.kemb[b * a.kemb_stride + c + j];
         }
         // every load first (the partials, then the residual), every store after:
@@ -371,7 +285,6 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float y = a.kbias ? v[k][j] + kb[j] : v[k][j];
-                    if (a.kbias2) y = y + kb2[j];   // a fused skip convolution's bias
                     if (a.kemb) y = y + ke[j];
                     if (kres) y = rs[k][j] + y;
                     v[k][j] = y;
@@ -504,12 +417,11 @@ __global__ __launch_bounds__(NT) void gn2_stats_kernel(GnArgs a) {
     const bool ksrc = a.kpart && c0 < a.C1;
     __shared__ double red[2][4 * NT];   // rows * Ctot = 4 * NT
     double s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-    f4 kb = {0.f, 0.f, 0.f, 0.f}, kb2 = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
+    f4 kb = {0.f, 0.f, 0.f, 0.f}, ke = {0.f, 0.f, 0.f, 0.f};
     if (ksrc) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (a.kbias) kb[j] = a.kbias[c0 + j];
-            if (a.kbias2) kb2[j] = a.kbias2[c0 + j];
             if (a.kemb) ke[j] = a.kemb[b * a.kemb_stride + c0 + j];
         }
     }
@@ -545,7 +457,6 @@ __global__ __launch_bounds__(NT) void gn2_stats_kernel(GnArgs a) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         float y = a.kbias ? v[u][j] + kb[j] : v[u][j];
-                        if (a.kbias2) y = y + kb2[j];
                         if (a.kemb) y = y + ke[j];
                         if (a.kres) y = rs[u][j] + y;
                         v[u][j] = y;
@@ -826,22 +737,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
     const int kt0 = bz * per;
     const int kt1 = min(nkt, kt0 + per);
     // wave-uniform K position of tile kt: (dy, dx) tap and channel base, in
-    // (tap, chunk) order or, with a.korder, (chunk, tap) order (the taps of one
-    // 32-channel chunk back to back re-read activation rows while they are in
-    // L2).  Derived from kt per tile and pinned to SGPRs: a position carried
-    // across tiles ended up in scratch and VGPRs, and a VGPR-selected buffer
-    // descriptor costs a readfirstlane loop around every load.
-    const int ntap_ = a.ks * a.ks;
+    // (tap, chunk) order.  Derived from kt per tile and pinned to SGPRs: a position
+    // carried across tiles ended up in scratch and VGPRs, and a VGPR-selected
+    // buffer descriptor costs a readfirstlane loop around every load.
     auto kpos_of = [&](int kt, int& cb, int& dy, int& dx) {
-        int tap;
-        if (a.korder) {
-            cb = BK * (kt / ntap_);
-            tap = kt - (kt / ntap_) * ntap_;
-        } else {
-            const int kb = kt * BK;
-            tap = kb / a.Ctot;
-            cb = kb - tap * a.Ctot;
-        }
+        const int kb = kt * BK;
+        const int tap = kb / a.Ctot;
+        cb = kb - tap * a.Ctot;
         dy = tap / a.ks;
         dx = tap - dy * a.ks;
         cb = __builtin_amdgcn_readfirstlane(cb);
@@ -1288,7 +1190,6 @@ __global__ void splitk_reduce_kernel(ConvArgs a, int splits) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         float y = a.bias ? s[j] + a.bias[n + j] : s[j];
-        if (a.bias2) y = y + a.bias2[n + j];   // a fused skip convolution's bias
         if (a.emb) y = y + a.emb[(int64_t)bb * a.emb_stride + n + j];
         if (a.res) y = rv[j] + y;
         v[j] = y;
@@ -1544,7 +1445,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 //   Vf[b][h][kb][dd][hl][lane][8]: channel 16 dd + lane%16, key 32 kb + kmap(lane/16, t)
 // with kmap(g, t) = 4g + t (t < 4), 16 + 4g + t - 4 (t >= 4): the keys a lane holds
 // of two 16-key S^T tiles, so P^T feeds the P.V MFMA straight from the softmax
-// registers.  attention_split_kernel then runs S^T = K Q^T and O^T = V^T P^T as
+// registers.  attention_dma_kernel (K4d) then runs S^T = K Q^T and O^T = V^T P^T as
 // three v_mfma_f32_16x16x32_f16 each (lo*hi + hi*lo + hi*hi, fp32 accumulate) over
 // 32-key blocks with the fp32 kernel's online softmax.  K carries the q/k scale
 // times log2(e) (kln2 below), so S is in base-2 units: every exponential is one
@@ -1599,147 +1500,15 @@ __global__ __launch_bounds__(256) void attn_kv_split_kernel(AttnArgs a, int CH, 
     dst[stride] = lo;
 }
 
-// QT query tiles of 16 per wave: every K / V fragment a wave loads feeds QT x
-// the MFMAs (QT = 2 halves the fragment traffic per FLOP where T is long enough
-// to keep 256 workgroups of 64 QT queries).
-template <int CH, int QT = 1>
-__global__ __launch_bounds__(256) void attention_split_kernel(AttnArgs a, const h8v* __restrict__ kf,
-                                                              const h8v* __restrict__ vf) {
-    constexpr int NJ = CH / 32;  // 32-deep k-chunks of the head dimension
-    constexpr int ND = CH / 16;  // 16-wide output blocks
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g = lane >> 4, li = lane & 15;
-    const int h = blockIdx.y, heads = gridDim.y;
-    const int64_t b = blockIdx.z;
-    const int T = a.T, T32 = (T + 31) / 32 * 32;
-    const int q0 = (blockIdx.x * 4 + wave) * 16 * QT;
-    if (q0 >= T) return;  // wave-uniform
-    CFD_DASSERT(h * CH + CH <= a.C);
-    const int C3 = 3 * a.C;
-    const float* base = a.qkv + b * (int64_t)T * C3 + (int64_t)h * 3 * CH;
-    const int64_t bh = b * heads + h;
-    const h8v* kfb = kf + bh * (T32 / 16) * NJ * 128 + lane;
-    const h8v* vfb = vf + bh * (T32 / 32) * ND * 128 + lane;
-
-    h8v qh[QT][NJ], ql[QT][NJ];
-#pragma unroll
-    for (int z = 0; z < QT; ++z) {
-        const int tq = min(q0 + 16 * z + li, T - 1);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const float* qp = base + (int64_t)tq * C3 + 32 * j + 8 * g;
-            float v[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) v[t] = qp[t] * a.scale;
-            split8_f16(v, qh[z][j], ql[z][j]);
-        }
-    }
-    f4 O[QT][ND];
-    float mrun[QT], lrun[QT];
-#pragma unroll
-    for (int z = 0; z < QT; ++z) {
-#pragma unroll
-        for (int d = 0; d < ND; ++d) O[z][d] = f4{0.f, 0.f, 0.f, 0.f};
-        mrun[z] = -INFINITY;
-        lrun[z] = 0.f;
-    }
-
-    for (int kb = 0; kb < T32; kb += 32) {
-        // S^T[key][query] of two 16-key tiles
-        f4 st[QT][2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-#pragma unroll
-            for (int z = 0; z < QT; ++z) st[z][u] = f4{0.f, 0.f, 0.f, 0.f};
-            const h8v* kp = kfb + (int64_t)((kb >> 4) + u) * NJ * 128;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const h8v kh = kp[j * 128], kl = kp[j * 128 + 64];
-#pragma unroll
-                for (int z = 0; z < QT; ++z) {
-                    st[z][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qh[z][j], st[z][u], 0, 0, 0);
-                    st[z][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, ql[z][j], st[z][u], 0, 0, 0);
-                    st[z][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[z][j], st[z][u], 0, 0, 0);
-                }
-            }
-        }
-        h8v ph[QT], pl[QT];
-#pragma unroll
-        for (int z = 0; z < QT; ++z) {
-            // lane (g, li) holds S[query li][key kb + 16u + 4g + r]
-            float mx = -INFINITY;
-            if (kb + 32 > T) {   // the ragged last block only (wave-uniform)
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (kb + 16 * u + 4 * g + r >= T) st[z][u][r] = -INFINITY;
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[z][u][r]);
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
-            const float mnew = fmaxf(mrun[z], mx);
-            const float alpha = __builtin_amdgcn_exp2f(mrun[z] - mnew);   // S in base-2 units
-            float p[8], ps = 0.f;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    p[4 * u + r] = __builtin_amdgcn_exp2f(st[z][u][r] - mnew);
-                    ps += p[4 * u + r];
-                }
-            ps += __shfl_xor(ps, 16);
-            ps += __shfl_xor(ps, 32);
-            lrun[z] = lrun[z] * alpha + ps;
-            mrun[z] = mnew;
-#pragma unroll
-            for (int d = 0; d < ND; ++d) O[z][d] = O[z][d] * alpha;
-            // element t of this lane's P^T operand is key kmap(g, t) = p[t]
-            split8_f16(p, ph[z], pl[z]);
-        }
-        // O^T[d][query] += V^T[d][key] P^T[key][query]
-        const h8v* vp = vfb + (int64_t)(kb >> 5) * ND * 128;
-#pragma unroll
-        for (int d = 0; d < ND; ++d) {
-            const h8v vh = vp[d * 128], vl = vp[d * 128 + 64];
-#pragma unroll
-            for (int z = 0; z < QT; ++z) {
-                O[z][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph[z], O[z][d], 0, 0, 0);
-                O[z][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl[z], O[z][d], 0, 0, 0);
-                O[z][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph[z], O[z][d], 0, 0, 0);
-            }
-        }
-    }
-    // lane (g, li) holds O[query li][16 d + 4 g + r]
-#pragma unroll
-    for (int z = 0; z < QT; ++z) {
-        const int tq = q0 + 16 * z + li;
-        if (a.lse && g == 0 && tq < T)   // natural units (the backward's exp(S - lse))
-            a.lse[((int64_t)b * gridDim.y + h) * T + tq] = (mrun[z] + log2f(lrun[z])) * 0.69314718055994530942f;
-        if (tq < T) {
-            float* op = a.out + (b * (int64_t)T + tq) * a.C + (int64_t)h * CH;
-            const float inv = 1.0f / lrun[z];
-#pragma unroll
-            for (int d = 0; d < ND; ++d) {
-                f4 v = O[z][d] * inv;
-                *(f4*)(op + 16 * d + 4 * g) = v;
-            }
-        }
-    }
-}
-
-// K4d: attention_split_kernel with each 32-key block's packed K/V fragments
+// K4d: the split attention, each 32-key block's packed K/V fragments
 // (attn_kv_split's layout: K of the block's two 16-key tiles = 4 NJ contiguous
 // 1-KiB pieces, V = 2 ND pieces) staged ONCE per workgroup into an NS-stage LDS
 // ring by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no VALU), NS - 1
-// blocks in flight, one barrier per block.  K4s has every wave stream the whole
-// K/V of its (sample, head) from L2 for its 16 queries (1 GB of L2 reads per
-// 32^2 attention at config B, the loop's bound: cutting its instruction count by
-// 45% left it unchanged); here WAVES waves share one copy.  Fragments, MFMA order
-// and softmax are K4s', so the output is bit-identical to it.
+// blocks in flight, one barrier per block; WAVES waves (16 queries each) share
+// one copy.  The round-2 form (K4s, removed in round 6) had every wave stream the
+// whole K/V of its (sample, head) from L2 (1 GB of L2 reads per 32^2 attention at
+// config B, its bound); K4d computes the same fragments in the same MFMA order
+// with the same softmax, bit-identical to it.
 template <int CH, int WAVES, int NS = 3>
 __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, const h8v* __restrict__ kf,
                                                                    const h8v* __restrict__ vf) {
@@ -1982,26 +1751,27 @@ static int env_int(const char* name, int dflt) {
 }
 
 // the two-launch full-row GroupNorm (gn2_*) for this shape (a function of the
-// per-sample shape only: batch invariance).  CFD_GN2_HW: from this many pixels
-// per sample up (0: never)
+// per-sample shape only: batch invariance): from 4096 pixels per sample at the
+// default plan.  Measured: B = 1 64^2 -3.5 %, config E -3 %, B = 8 flat; the
+// threshold scales with the planned batch (plan_b 2: from 1024 pixels, where the
+// one-launch kernels' 32 workgroups per sample leave a batch-1 chip idle)
 bool gn2_applies(const GnArgs& a) {
-    // measured: B = 1 64^2 -3.5 %, config E -3 %, B = 8 flat; the threshold scales
-    // with the planned batch (plan_b 2: from 1024 pixels, where the one-launch
-    // kernels' 32 workgroups per sample leave a batch-1 chip idle)
-    static const int hw = env_int("CFD_GN2_HW", 4096);
     const int pb = a.plan_b > 0 ? a.plan_b : 8;
-    return hw > 0 && (int64_t)a.HW * 8 >= (int64_t)hw * pb && a.Ctot % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0 &&
+    return (int64_t)a.HW * 8 >= (int64_t)4096 * pb && a.Ctot % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0 &&
            a.Ctot <= 1024;
+}
+
+// rows of the register-resident kernel's (pixel, channel-quad) grid per pass and
+// pixels per thread (0: not that kernel's shape)
+static int gn_reg_ipt(const GnArgs& a) {
+    return a.Ctot % 128 == 0 ? (int)ceil_div(a.HW, 512 / (a.Ctot / 128)) : 0;
 }
 
 bool gn_takes_splitk(const GnArgs& a, int B) {
     (void)B;
     if (gn2_applies(a)) return a.C1 % 4 == 0;
-    static const int fused = env_int("CFD_GN_FUSED", 1);
-    static const int ksrc = env_int("CFD_GN_SPLITK", 1);
-    if (!ksrc || fused != 1 || a.Ctot % 128 != 0 || a.C1 % 4 != 0) return false;
-    const int rows = 512 / (a.Ctot / 128);
-    return ceil_div(a.HW, rows) <= 16;
+    if (a.Ctot % 128 != 0 || a.C1 % 4 != 0) return false;
+    return gn_reg_ipt(a) <= 16;
 }
 
 void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
@@ -2028,32 +1798,23 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
         check_launch("gn2_apply_kernel");
         return;
     }
-    static const int fused = env_int("CFD_GN_FUSED", 1);
-    static const int big = env_int("CFD_GN_BIG", 1);   // 0: the one-launch kernels at every size
-    static const int nt1024 = env_int("CFD_GN_NT1024", 1);
-    const int ipt = a.Ctot % 128 == 0 ? (int)ceil_div(a.HW, 512 / (a.Ctot / 128)) : 0;
-    // large latents (ipt > 32): a workgroup per (sample, group) would leave the
-    // chip idle at small batch (32 workgroups at B = 1, 384^2), so they take the
-    // three-kernel path below, whose statistics spread over gn_chunks(HW) chunks
-    if (fused && a.Ctot % 128 == 0 && !(big && ipt > 32 && fused != 2)) {
+    // one workgroup per (sample, group), the sample's rows in registers; 1024
+    // threads up to 16 pixels per thread (twice the waves, and loads, in flight per
+    // CU).  Large latents (ipt > 32) would leave the chip idle at small batch (32
+    // workgroups at B = 1, 384^2): they take the three-kernel path below, whose
+    // statistics spread over gn_chunks(HW) chunks
+    const int ipt = gn_reg_ipt(a);
+    if (ipt > 0 && ipt <= 32) {
         const dim3 grid((unsigned)(32 * B));
-        if (fused == 2 || ipt > 32)
-            hipLaunchKernelGGL(gn_fused_kernel, grid, dim3(256), 0, st, a);
-        else if (nt1024 && ipt <= 4)   // 1024 threads: twice the waves (and loads) in flight per CU
+        if (ipt <= 4)
             hipLaunchKernelGGL((gn_fused_reg_kernel<2, 1024>), grid, dim3(1024), 0, st, a);
-        else if (nt1024 && ipt <= 8)
-            hipLaunchKernelGGL((gn_fused_reg_kernel<4, 1024>), grid, dim3(1024), 0, st, a);
-        else if (nt1024 && ipt <= 16)
-            hipLaunchKernelGGL((gn_fused_reg_kernel<8, 1024>), grid, dim3(1024), 0, st, a);
-        else if (ipt <= 4)
-            hipLaunchKernelGGL(gn_fused_reg_kernel<4>, grid, dim3(512), 0, st, a);
         else if (ipt <= 8)
-            hipLaunchKernelGGL(gn_fused_reg_kernel<8>, grid, dim3(512), 0, st, a);
+            hipLaunchKernelGGL((gn_fused_reg_kernel<4, 1024>), grid, dim3(1024), 0, st, a);
         else if (ipt <= 16)
-            hipLaunchKernelGGL(gn_fused_reg_kernel<16>, grid, dim3(512), 0, st, a);
+            hipLaunchKernelGGL((gn_fused_reg_kernel<8, 1024>), grid, dim3(1024), 0, st, a);
         else
             hipLaunchKernelGGL(gn_fused_reg_kernel<32>, grid, dim3(512), 0, st, a);
-        check_launch("gn_fused_kernel");
+        check_launch("gn_fused_reg_kernel");
         return;
     }
     hipLaunchKernelGGL(gn_partial_kernel, dim3(a.nchunks, B), dim3(256), 0, st, a);
@@ -2075,120 +1836,93 @@ static int even_splits(int nch, int splits) {
 }
 
 ConvPlan plan_conv(const ConvArgs& a, size_t part_cap_floats) {
-    // Every choice is made from the per-sample shape (as if the batch were 8),
-    // never from the actual batch: the split-K count fixes each output's
-    // summation order, so a sample's eps is then bit-identical whatever batch
-    // (or rank shard) it is computed in.  Knobs (development): CFD_CONV_BM
-    // (0 = auto), CFD_CONV_TARGET_WG.
-    static const int force_bm = env_int("CFD_CONV_BM", 0);
-    static const int target = env_int("CFD_CONV_TARGET_WG", 768);
-    // development: CFD_PLAN_B plans for that batch instead of 8 (small-batch experiments)
-    static const int plan_b_env = env_int("CFD_PLAN_B", 8);
-    // part_cap_floats: the split-K slab per planned batch (the caller sizes the real
-    // slab as ceil(B / plan_b) of these)
-    const int plan_b = a.plan_b > 0 ? a.plan_b : plan_b_env;
+    // Every choice is made from the per-sample shape at the planned batch (8 unless
+    // the model sets another, cfd_unet_set_plan_batch), never from the actual
+    // batch: the split-K count fixes each output's summation order, so a sample's
+    // eps is then bit-identical whatever batch (or rank shard) it is computed in.
+    // part_cap_floats: the split-K slab per planned batch (the caller sizes the
+    // real slab as ceil(B / plan_b) of these)
+    const int plan_b = a.plan_b > 0 ? a.plan_b : 8;
     ConvPlan p;
     const int64_t mn = (int64_t)plan_b * a.Hout * a.Wout;
     p.bn = a.Cout >= 128 ? 128 : 64;
     auto tiles = [&](int bm) { return ceil_div(mn, bm) * ceil_div(a.Cout, p.bn); };
-    p.bm = force_bm ? force_bm : 64;  // 64x128 measured ahead of 128x128 (r01 sweep: 8.76 vs 9.26 ms)
-    // 8-wave 128x128 tiles for Cout >= 128 (CFD_CONV_NW8: 2 = everywhere, 1 = where
-    // they fill the chip without split-K, 0 = never), counted as 2 WGs each.
-    // Measured B=8 64^2 forward: 5.88 ms (0), 5.69 (1), 5.51 (2, 1024-WG target).
-    static const int nw8 = env_int("CFD_CONV_NW8", 2);
+    // K1s tiles: 8-wave 128x128 for Cout >= 128, counted as 2 workgroups each (r01
+    // sweep, B = 8 64^2 forward: 5.51 ms vs 5.88 with 4-wave tiles), else 64x64;
+    // split-K up to a 768-workgroup target, >= 4 K tiles per split
+    p.bm = 64;
     int wg_per_tile = 1;
-    if (!force_bm && p.bn == 128 && (nw8 == 2 || (nw8 == 1 && tiles(128) >= 256))) {
+    if (p.bn == 128) {
         p.bm = 128;
         p.nw = 8;
         wg_per_tile = 2;
     }
     const int nkt = a.K / 32;
     p.splits = 1;
-    while (tiles(p.bm) * wg_per_tile * p.splits < target && nkt / (p.splits * 2) >= 4 && p.splits < 16)
+    while (tiles(p.bm) * wg_per_tile * p.splits < 768 && nkt / (p.splits * 2) >= 4 && p.splits < 16)
         p.splits *= 2;
     // 1x1 convolutions (qkv, proj_out, skip) with >= 128 tiles: no split-K.  Their
     // K is short (256-640), so a split only adds partial slabs and a reduction pass
     // (convbench, reduction included: 1.09-1.72x unsplit on the config-B shapes
-    // with 128-256 tiles, 0.5-0.8x below; CFD_CONV_1X1_SPLIT=1 restores the target)
-    static const int split1x1 = env_int("CFD_CONV_1X1_SPLIT", 0);
-    if (!split1x1 && a.ks == 1 && !a.tmode && tiles(p.bm) >= 128) p.splits = 1;
-    // memory guard, on the nominal shape too: part_cap_floats is the slab per 8
-    // samples (the caller sizes the real slab as ceil(B/8) of these)
+    // with 128-256 tiles, 0.5-0.8x below)
+    if (a.ks == 1 && !a.tmode && tiles(p.bm) >= 128) p.splits = 1;
+    // memory guard, on the nominal shape too
     while (p.splits > 1 && (size_t)p.splits * mn * a.Cout > part_cap_floats) p.splits /= 2;
-    // the large-latent levels (Case4's 192^2 / 384^2) with <= 128 input channels:
-    // K1s 128x128 tiles of 8 waves (tools/convbench at one sample: 384^2 128->128
-    // 178 vs K1h 199 us, the 2x upsampling 174 vs 197, 192^2 128->128 63 vs 74;
-    // 256 input channels stay on K1h: 344 vs 364 us)
-    static const int k1s_big = env_int("CFD_CONV_K1S_HW", 36864);
-    if (k1s_big > 0 && a.wlo && a.ks == 3 && a.stride == 1 && !a.tmode && a.Ctot <= 128 &&
-        (int64_t)a.Hout * a.Wout >= k1s_big)
+    // the large-latent levels (Case4's 192^2 / 384^2) with <= 128 input channels
+    // stay on the K1s 128x128 8-wave tiles (tools/convbench at one sample: 384^2
+    // 128->128 178 vs K1h 199 us, the 2x upsampling 174 vs 197, 192^2 128->128 63
+    // vs 74; 256 input channels go to K1h: 344 vs 364 us)
+    if (a.wlo && a.ks == 3 && a.stride == 1 && !a.tmode && a.Ctot <= 128 && (int64_t)a.Hout * a.Wout >= 36864)
         return p;
-    // K1x (conv_x.hip) for the split-f16 3x3 stride-1 convolutions: 64x64 wave
-    // tiles on 32x32x16 MFMAs; 256x128 workgroup tiles where the per-sample shape
-    // has >= 256 pixels at batch 8, 128x128 / 4 waves below (tools/convbench:
-    // 1.04-1.11x / 1.17x the K1s tiles on the config-B shapes, same box)
-    static const int kx = env_int("CFD_CONV_KX", 1);
-    // CFD_CONV_KX1 (development): K1x also for the 1x1 and stride-2 convolutions
-    static const int kx1 = env_int("CFD_CONV_KX1", 0);
-    const bool kx_shape = (a.ks == 3 && a.stride == 1) || (kx1 && !a.up && (a.ks == 1 || a.stride == 2));
     const int64_t srows = mn / ((int64_t)a.Hout * a.Wout) * a.Hin * a.Win;
-    // K1hb (conv_x.hip): the bf16-operand convolutions (config E) on the halo tiles
-    static const int khb = env_int("CFD_CONV_KHB", 1);
-    if (khb && kx && a.wbf && !a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 &&
-        srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31) &&
-        conv_h_tw(a) > 0) {
+    const bool fits32 = srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) &&
+                        (int64_t)a.Cout * a.K * 2 < (1ll << 31);
+    auto halo_splits = [&](int64_t t) {   // K1h / K1hb: split-K over the 32-channel chunks
+        const int nch = a.Ctot / 32;
+        int sp = 1;
+        while (t * sp < 256 && sp * 2 <= nch && sp < 16) sp *= 2;
+        while (sp > 1 && (size_t)sp * mn * a.Cout > part_cap_floats) sp /= 2;
+        return even_splits(nch, sp);
+    };
+    // K1hb (conv_x.hip): the bf16-operand 3x3 convolutions (config E) on the halo
+    // tiles; the others (8^2, which the 256-pixel tiles do not cover) stay on the
+    // K1s bf16 tiles
+    if (a.wbf && !a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 && fits32 && conv_h_tw(a) > 0) {
         ConvPlan q;
         q.kx = 22;
         q.bm = 256;
         q.bn = 128;
         q.nw = 8;
-        const int64_t t = ceil_div(mn, 256) * ceil_div(a.Cout, 128);
-        const int nch = a.Ctot / 32;
-        q.splits = 1;
-        while (t * q.splits < 256 && q.splits * 2 <= nch && q.splits < 16) q.splits *= 2;
-        while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
-        q.splits = even_splits(nch, q.splits);
+        q.splits = halo_splits(ceil_div(mn, 256) * ceil_div(a.Cout, 128));
         return q;
     }
-    // K1x with bf16 operands (config E's 8^2 3x3 convolutions, which K1hb's 256-pixel
-    // halo tiles do not cover; CFD_CONV_KXB=1, off by default: K1s bf16 tiles)
-    static const int kxb = env_int("CFD_CONV_KXB", 0);   // measured: config E 4.70 vs 4.68 ms per step off (same box)
-    const bool bf_kx = kxb && a.wbf && !a.wlo && a.ks == 3 && a.stride == 1;
-    if (kx && a.wbf && (a.wlo || bf_kx) && !a.tmode && kx_shape && a.Cout >= 128 &&
-        srows < (1 << 23) && srows * std::max(a.C1, a.C2) * 4 < (1ll << 30) && (int64_t)a.Cout * a.K * 2 < (1ll << 31)) {
+    // the split-f16 3x3 stride-1 convolutions: K1h (halo tiles) where a 256-pixel
+    // block tiles the image (16x16 and up: each activation fetched once per
+    // 32-channel chunk instead of once per tap; tools/convbench, same box:
+    // 1.19-1.29x K1x on the config-B 64^2 / 32^2 shapes, 1.04-1.17x at 16^2), else
+    // K1x: 64x64 wave tiles on 32x32x16 MFMAs, 256x128 workgroup tiles where the
+    // per-sample shape has >= 256 pixels at the planned batch, 128x128 below
+    // (1.04-1.17x the K1s tiles).  1x1 and stride-2 convolutions stay on K1s.
+    if (a.wbf && a.wlo && !a.tmode && a.ks == 3 && a.stride == 1 && a.Cout >= 128 && fits32) {
         ConvPlan q;
-        // K1h (halo tiles, conv_x.hip) where a 256-pixel block tiles the image
-        // (16x16 and up): each activation fetched once per 32-channel chunk
-        // instead of once per tap (tools/convbench, same box: 1.19-1.29x K1x on
-        // the config-B 64^2/32^2 shapes, 1.04-1.17x at 16^2 with split-K 8);
-        // split-K over the chunks, at least one chunk per split
-        static const int kh = env_int("CFD_CONV_KH", 1);
-        if (kh && a.wlo && a.ks == 3 && a.stride == 1 && conv_h_tw(a) > 0) {
+        if (conv_h_tw(a) > 0) {
             q.kx = 20;
             q.bm = 256;
             q.bn = 128;
             q.nw = 8;
-            const int64_t t = ceil_div(mn, 256) * ceil_div(a.Cout, 128);
-            const int nch = a.Ctot / 32;
-            q.splits = 1;
-            while (t * q.splits < 256 && q.splits * 2 <= nch && q.splits < 16) q.splits *= 2;
-            while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
-            q.splits = even_splits(nch, q.splits);
+            q.splits = halo_splits(ceil_div(mn, 256) * ceil_div(a.Cout, 128));
             return q;
         }
-        // at least CFD_CONV_KMIN (4) K tiles per split, at most CFD_CONV_SMAX (32)
-        // splits: the small levels (8^2, 4^2) run long K chains on few tiles, and
-        // at batch 1 each K tile waits a memory latency (config A 32^2 B=1 forward
-        // 2.78 -> 2.68 ms against 8 / 16; B=8 64^2 unchanged)
-        static const int kmin = env_int("CFD_CONV_KMIN", 4);
-        static const int smax = env_int("CFD_CONV_SMAX", 32);
+        // at least 4 K tiles per split, at most 32 splits: the small levels (8^2,
+        // 4^2) run long K chains on few tiles, and at batch 1 each K tile waits a
+        // memory latency (config A 32^2 B = 1 forward 2.78 -> 2.68 ms against 8 / 16)
         q.kx = mn >= 2048 ? 2 : 1;
         q.bm = q.kx == 2 ? 256 : 128;
         q.bn = 128;
         q.nw = q.kx == 2 ? 8 : 4;
         const int64_t t = ceil_div(mn, q.bm) * ceil_div(a.Cout, q.bn);
         q.splits = 1;
-        while (t * q.splits < 256 && nkt / (q.splits * 2) >= kmin && q.splits < smax) q.splits *= 2;
+        while (t * q.splits < 256 && nkt / (q.splits * 2) >= 4 && q.splits < 32) q.splits *= 2;
         while (q.splits > 1 && (size_t)q.splits * mn * a.Cout > part_cap_floats) q.splits /= 2;
         return q;
     }
@@ -2259,26 +1993,11 @@ static bool conv_x_falls_back(const ConvArgs& a) {
 
 bool conv_runs_k1hb(const ConvArgs& a, const ConvPlan& p) { return p.kx == 22 && !conv_x_falls_back(a); }
 
-bool conv_takes_skip(const ConvArgs& a, const ConvPlan& p) {
-    static const int khg = env_int("CFD_CONV_KHG", 0);
-    const int XC = a.XC1 + a.XC2;
-    const bool kgroups = p.kx == 20 && p.splits == 2 && khg > 0 && a.Cout % 64 == 0 &&
-                         ceil_div(a.M, 256) * ceil_div(a.Cout, 64) >= khg;   // launch_conv's variant 24
-    // K1h only: the K1x form (conv_x_kernel<..., XF>) is built but keeps part of its
-    // arguments in scratch (measured first: CFD_CONV_SKIPFUSE=2 also takes it)
-    static const int kx_too = env_int("CFD_CONV_SKIPFUSE", 0) == 2;
-    return (p.kx == 20 || (kx_too && (p.kx == 1 || p.kx == 2))) && !kgroups && !conv_x_falls_back(a) && a.wbf && a.wlo &&
-           a.xwbf && a.xwlo && !a.tmode && !a.up && a.ks == 3 && a.stride == 1 && !a.src_bf16 && XC > 0 &&
-           XC % 32 == 0 && a.XC1 % 4 == 0 && a.XC2 % 4 == 0 && (int64_t)a.M * std::max(a.XC1, a.XC2) * 4 < (1ll << 31) &&
-           (int64_t)a.Cout * XC * 2 < (1ll << 31) && (p.kx != 20 || conv_h_tw(a) > 0);
-}
-
 bool conv_kv_pack_ok(const ConvArgs& a, const ConvPlan& p, int T) {
-    // launch_conv's choices: K1s (a 1x1 never takes K1x unless CFD_CONV_KX1), split or
-    // bf16 compute (MODE 2 / 1: bands of whole 32-row blocks), the LDS epilogue on, one split
+    // launch_conv's choices: K1s (a 1x1 never takes K1x), split or bf16 compute
+    // (MODE 2 / 1: bands of whole 32-row blocks), the LDS epilogue on, one split
     static const int ldsepi = env_int("CFD_CONV_LDSEPI", 1);
-    static const int fuse = env_int("CFD_ATTN_KVFUSE", 1);   // 0: the attn_kv_split launch (A/B)
-    return fuse && ldsepi && p.kx < 0 && p.splits == 1 && a.wbf && !a.tmode && a.ks == 1 && a.bias &&
+    return ldsepi && p.kx < 0 && p.splits == 1 && a.wbf && !a.tmode && a.ks == 1 && a.bias &&
            !a.emb && !a.res && a.Cout % 8 == 0 && a.emb_stride % 4 == 0 && T % 32 == 0 && a.M % T == 0;
 }
 
@@ -2296,15 +2015,12 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     static const int pf = env_int("CFD_CONV_PF", 2);
     if (p.kx < 0) p.pf = pf >= 1 && pf <= 3 ? pf : 1;
     CFD_REQUIRE(a.Ctot % 32 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0, CFD_ESHAPE, "conv_gemm needs channels % 32 == 0");
-    CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot + a.XC1 + a.XC2, CFD_ESHAPE, "conv K mismatch");
-    CFD_REQUIRE(!a.xsrc1 || conv_takes_skip(a, p0), CFD_ESTATE, "internal: fused skip convolution on an ineligible plan");
+    CFD_REQUIRE(a.K == a.ks * a.ks * a.Ctot, CFD_ESHAPE, "conv K mismatch");
     CFD_REQUIRE(p.splits == 1 || (a.part && a.Cout % 4 == 0), CFD_ESTATE, "split-K needs a partial buffer");
     CFD_REQUIRE(!a.tmode || ((a.stride == 1 || a.stride == 2) && !a.up), CFD_ESHAPE, "transposed conv: stride 1|2");
     const dim3 grid((unsigned)ceil_div(a.M, p.bm), (unsigned)ceil_div(a.Cout, p.bn), p.splits);
     CFD_REQUIRE(!(a.tmode && a.wbf && !a.wlo), CFD_ESTATE, "bf16 input-gradient convolutions are not built");
     static const int xcd = env_int("CFD_CONV_XCD", 4);   // round 5: 3 (PMC: 16^2 K1h L2 hit 0.19-0.27 -> 0.69-0.79), then 4
-    static const int korder = env_int("CFD_CONV_KORDER", 0);
-    static const int bufaddr = env_int("CFD_CONV_BUFADDR", 1);
     static const int ldsepi = env_int("CFD_CONV_LDSEPI", 1);
     ConvArgs b = a;
     b.stamps = g_stamps;
@@ -2317,24 +2033,13 @@ int launch_conv(const ConvArgs& a, const ConvPlan& p0, hipStream_t st, bool defe
     // split-f16 config A is 0.3 % slower with it, r05as), 3 for the others
     const int xo = xcd == 4 ? (a.wbf && !a.wlo ? 1 : 3) : xcd;
     b.xcd = xo == 3 ? ((int64_t)a.Hout * a.Wout <= 256 ? 2 : 1) : xo < 0 || xo > 2 ? 1 : xo;
-    b.korder = korder ? 1 : 0;
     {   // 32-bit buffer offsets and 24-bit pixel indices must hold
         const int64_t srows = (int64_t)a.Hin * a.Win * (a.M / (a.Hout * a.Wout));
         const int64_t wes = (a.wbf || a.wlo) ? 2 : 4;
-        b.bufaddr = bufaddr && a.ks * a.ks <= 9 && srows < (1 << 24) && a.M < (1 << 24) &&
+        b.bufaddr = a.ks * a.ks <= 9 && srows < (1 << 24) && a.M < (1 << 24) &&
                     srows * std::max(a.C1, a.C2) * 4 < (1ll << 31) && (int64_t)a.Cout * a.K * wes < (1ll << 31);
     }
     const ConvArgs& a_ = b;
-    // K1h / K1hb split-K 2 as two in-workgroup K groups (conv_x.hip): the same
-    // chunk ranges and combination order, so the same bits, without the partial
-    // slab and its reduction pass; where the grid keeps >= CFD_CONV_KHG workgroups
-    // (0: never)
-    static const int khg = env_int("CFD_CONV_KHG", 0);
-    if ((p.kx == 20 || p.kx == 22) && p.splits == 2 && khg > 0 && a.Cout % 64 == 0 &&
-        ceil_div(a.M, 256) * ceil_div(a.Cout, p.kx == 20 ? 64 : 128) >= khg) {
-        launch_conv_x(a_, p.kx + 4, 1, st);
-        return 1;
-    }
     if (p.kx >= 0) {
         launch_conv_x(a_, p.kx, p.splits, st);
         if (p.splits > 1 && !defer) launch_splitk_reduce(a, p.splits, st);
@@ -2413,42 +2118,25 @@ void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* 
                            B, kf, vf);
         check_launch("attn_kv_split_kernel");
     }
-    // K4d (default; CFD_ATTN_DMA=0 restores K4s): fragments staged per workgroup
-    // by LDS-DMA, 8 waves (128 queries) per workgroup where T >= 512 and that still
-    // gives >= 256 workgroups, else 4 -- at batch 1 the 64-query workgroups double
-    // the parallelism of the 32^2 blocks (the choice changes no result: every
-    // query's arithmetic is the same)
-    static const int dma = env_int("CFD_ATTN_DMA", 1);
+    // K4d: fragments staged per workgroup by LDS-DMA, 8 waves (128 queries) per
+    // workgroup where T >= 512 and that still gives >= 256 workgroups, else 4 -- at
+    // batch 1 the 64-query workgroups double the parallelism of the 32^2 blocks
+    // (the choice changes no result: every query's arithmetic is the same)
     static const int xcdmap = env_int("CFD_ATTN_XCD", 1);   // (sample, head) workgroups on one XCD
-    if (dma) {
-        AttnArgs a2 = a;
-        a2.xcdmap = xcdmap && (heads * B) % 8 == 0 ? 1 : 0;
-        const AttnArgs& a = a2;
-        const int w8 = a.T >= 512 && (int64_t)B * heads * ceil_div(a.T, 128) >= 256;
-        const dim3 grid((unsigned)ceil_div(a.T, w8 ? 128 : 64), heads, B);
-        const dim3 blk(w8 ? 512 : 256);
-        switch (CH * 2 + w8) {
-            case 64: hipLaunchKernelGGL((attention_dma_kernel<32, 4>), grid, blk, 0, st, a, kf, vf); break;
-            case 65: hipLaunchKernelGGL((attention_dma_kernel<32, 8>), grid, blk, 0, st, a, kf, vf); break;
-            case 128: hipLaunchKernelGGL((attention_dma_kernel<64, 4>), grid, blk, 0, st, a, kf, vf); break;
-            case 129: hipLaunchKernelGGL((attention_dma_kernel<64, 8>), grid, blk, 0, st, a, kf, vf); break;
-            case 256: hipLaunchKernelGGL((attention_dma_kernel<128, 4>), grid, blk, 0, st, a, kf, vf); break;
-            default: hipLaunchKernelGGL((attention_dma_kernel<128, 8>), grid, blk, 0, st, a, kf, vf); break;
-        }
-        check_launch("attention_dma_kernel");
-        return;
+    AttnArgs a2 = a;
+    a2.xcdmap = xcdmap && (heads * B) % 8 == 0 ? 1 : 0;
+    const int w8 = a.T >= 512 && (int64_t)B * heads * ceil_div(a.T, 128) >= 256;
+    const dim3 grid((unsigned)ceil_div(a.T, w8 ? 128 : 64), heads, B);
+    const dim3 blk(w8 ? 512 : 256);
+    switch (CH * 2 + w8) {
+        case 64: hipLaunchKernelGGL((attention_dma_kernel<32, 4>), grid, blk, 0, st, a2, kf, vf); break;
+        case 65: hipLaunchKernelGGL((attention_dma_kernel<32, 8>), grid, blk, 0, st, a2, kf, vf); break;
+        case 128: hipLaunchKernelGGL((attention_dma_kernel<64, 4>), grid, blk, 0, st, a2, kf, vf); break;
+        case 129: hipLaunchKernelGGL((attention_dma_kernel<64, 8>), grid, blk, 0, st, a2, kf, vf); break;
+        case 256: hipLaunchKernelGGL((attention_dma_kernel<128, 4>), grid, blk, 0, st, a2, kf, vf); break;
+        default: hipLaunchKernelGGL((attention_dma_kernel<128, 8>), grid, blk, 0, st, a2, kf, vf); break;
     }
-    // K4s (CFD_ATTN_DMA=0): every wave streams its (sample, head)'s fragments from
-    // L2 (K4s2, K/V staged per block in LDS without a pack kernel, and two query
-    // tiles per wave measured slower and were removed in round 3)
-    const dim3 grid((unsigned)ceil_div(a.T, 64), heads, B);
-    switch (CH) {
-        case 32: hipLaunchKernelGGL((attention_split_kernel<32, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
-        case 64: hipLaunchKernelGGL((attention_split_kernel<64, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
-        case 128: hipLaunchKernelGGL((attention_split_kernel<128, 1>), grid, dim3(256), 0, st, a, kf, vf); break;
-        default: throw Error{CFD_ESHAPE, "split attention head channels must be 32, 64 or 128"};
-    }
-    check_launch("attention_split_kernel");
+    check_launch("attention_dma_kernel");
 }
 
 void launch_temb(const int64_t* t, const float* freqs, float* out, int dim, int B, hipStream_t st) {

@@ -27,7 +27,6 @@ struct GnArgs {
     const float* kbias;
     const float* kemb;
     const float* kres;
-    const float* kbias2;  // a fused skip convolution's bias (ConvArgs::bias2), or null
     float* kx;           // where the reduced sum is stored (null: nowhere, nobody reads it)
     int ksplits, kemb_stride;
     unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
@@ -65,7 +64,6 @@ struct ConvArgs {
     int emb_stride;
     int M, K;
     int xcd;             // XCD-contiguous workgroup order (set by launch_conv; CFD_CONV_XCD=0: off)
-    int korder;          // K tile order: 0 (tap, channel chunk), 1 (channel chunk, tap) (set by launch_conv)
     int bufaddr;         // 32-bit buffer addressing of the operands (set by launch_conv where it fits)
     int ldsepi;          // K1s: epilogue through LDS, float4 rows (set by launch_conv; CFD_CONV_LDSEPI=0: off)
     int* nonfinite;      // conv_out only: set to 1 when an output is not finite (range guard), or null
@@ -77,22 +75,9 @@ struct ConvArgs {
     int64_t kv_voff;
     int kv_ch, kv_heads, kv_T;
     float kv_scale;      // the attention's q / k scale (K carries scale * log2 e)
-    // fused 1x1 skip convolution (a ResBlock's out_layers in split compute, on K1h /
-    // K1x: conv_takes_skip): XC1 + XC2 more K channels of the raw block input (two
-    // sources, read at the output pixel), weights xwbf / xwlo (Cout, XC1 + XC2) f16
-    // hi / lo, its bias in bias2.  The two weight packs carry their own power-of-two
-    // scales; main_scale / x_scale (powers of two <= 1, exact) scale the operands as
-    // they are staged so both parts accumulate at the scale acc_scale undoes
-    const float* xsrc1;
-    const float* xsrc2;
-    int XC1, XC2;
-    const void* xwbf;
-    const void* xwlo;
-    const float* bias2;
-    float main_scale, x_scale;
     unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
     int seq;                      // launch sequence number (timestamps)
-    // the batch plan_conv tiles for (0: 8, or CFD_PLAN_B): a per-model setting
+    // the batch plan_conv tiles for (0: 8): a per-model setting
     // (cfd_unet_set_plan_batch), never the real batch, so a sample's sums do not
     // depend on the batch it runs in
     int plan_b;
@@ -235,9 +220,6 @@ int64_t attention_split_voff(int T, int CH, int heads, int B);
 // whether launch_conv runs this qkv plan through a K1s LDS epilogue that can pack
 // the K / V fragments (split compute, no split-K, T % 32 == 0)
 bool conv_kv_pack_ok(const ConvArgs& a, const ConvPlan& p, int T);
-// whether this 3x3 plan can take a fused 1x1 skip convolution (ConvArgs::xsrc1):
-// K1h (256-pixel halo tiles) or K1x in split compute, no fallback to K1s
-bool conv_takes_skip(const ConvArgs& a, const ConvPlan& p);
 // backward (unet_vjp.hip)
 int launch_gn_bwd(const GnbArgs& a, int B, hipStream_t st);   // returns the pixel chunks used
 void launch_attention_bwd(const AttnBwdArgs& a, int CH, int heads, int B, hipStream_t st);

@@ -778,10 +778,9 @@ namespace {
 bool wgrad_fast(const WgradArgs& a) {
     return a.Ctot % 128 == 0 && a.Cout % 4 == 0 && a.C1 % 4 == 0 && a.C2 % 4 == 0;
 }
-// conv_wgrad_thin_kernel's shapes (CFD_WGRAD_THIN=0: the 64-tile kernel)
+// conv_wgrad_thin_kernel's shapes (the 1- to 4-channel convolutions)
 bool wgrad_thin(const WgradArgs& a) {
-    static const int on = getenv("CFD_WGRAD_THIN") ? atoi(getenv("CFD_WGRAD_THIN")) : 1;
-    return on && !wgrad_fast(a) && (a.Ctot <= 4 || a.Cout <= 4) && a.stride == 1 && !a.up && a.ks <= 3 &&
+    return !wgrad_fast(a) && (a.Ctot <= 4 || a.Cout <= 4) && a.stride == 1 && !a.up && a.ks <= 3 &&
            a.Hin == a.Hout && a.Win == a.Wout;
 }
 }  // namespace
@@ -796,11 +795,8 @@ int64_t wgrad_kspan(const WgradArgs& a) {
         const int64_t tiles = ceil_div(N, 128) * ceil_div(a.Cout, 128);
         // as many slices as fill whole rounds of resident blocks: 512 = two 64-KB-LDS
         // blocks per CU, so a launch has no partial last round (576 blocks, 9 tiles
-        // x 64 slices, ran as two rounds, the second one eighth full).  Development:
-        // CFD_WGRAD_SMAX / CFD_WGRAD_TARGET (slices at most / blocks at most)
-        static const int smax = getenv("CFD_WGRAD_SMAX") ? atoi(getenv("CFD_WGRAD_SMAX")) : 64;
-        static const int target = getenv("CFD_WGRAD_TARGET") ? atoi(getenv("CFD_WGRAD_TARGET")) : 512;
-        splits = std::min<int64_t>({(int64_t)smax, std::max<int64_t>(1, target / tiles), ceil_div(a.P, 256),
+        // x 64 slices, ran as two rounds, the second one eighth full); at most 64 slices
+        splits = std::min<int64_t>({(int64_t)64, std::max<int64_t>(1, 512 / tiles), ceil_div(a.P, 256),
                                     std::max<int64_t>(1, a.part_cap / MN)});
         splits = std::max<int64_t>(1, splits);
         const int64_t span = ceil_div(a.P, splits);
@@ -835,11 +831,11 @@ bool launch_conv_wgrad(WgradArgs a, float* G, hipStream_t st) {
     CFD_REQUIRE(wgrad_part_floats(a) <= (size_t)a.part_cap, CFD_ESTATE, "internal: weight-gradient scratch");
     if (wgrad_fast(a)) {
         CFD_REQUIRE(a.P < (int64_t)1 << 31, CFD_ESHAPE, "weight gradient over 2^31 or more pixels");
-        // split-f16 products (CFD_WGRAD_SPLIT=0: the exact fp32-MFMA kernel)
-        static const int split_env = getenv("CFD_WGRAD_SPLIT") ? atoi(getenv("CFD_WGRAD_SPLIT")) : 1;
-        // fdiv24 pixel decode; 32-bit element offsets; one source per 128-column tile
+        // split-f16 products where the operand ranges are known (else the exact
+        // fp32-MFMA kernel); fdiv24 pixel decode; 32-bit element offsets; one source
+        // per 128-column tile
         const int64_t srows0 = (int64_t)(a.P / ((int64_t)a.Hout * a.Wout)) * a.Hin * a.Win;
-        const bool split = split_env && a.amax_y && a.amax_x && a.P < (1 << 24) && a.P * a.Cout < (1ll << 31) &&
+        const bool split = a.amax_y && a.amax_x && a.P < (1 << 24) && a.P * a.Cout < (1ll << 31) &&
                            srows0 * a.Ctot < (1ll << 31) && (a.ss || a.C2 == 0 || a.C1 % 128 == 0);
         auto absmax = [&](const float* x, int64_t n, unsigned* out) {
             const int64_t n4 = n / 4;

@@ -1017,28 +1017,19 @@ int launch_gn_bwd(const GnbArgs& a0, int B, hipStream_t st) {
                                             std::max<int64_t>(1, ceil_div(a.HW, 16 * rows))});
     } else {
         // no parameter partials (the DPS adjoint): gn2's chunking, the statistics
-        // finalised inside the apply pass, up to 128^2 (CFD_GNB2=0: the finalize
-        // launch, A/B; 2: also beyond, where every apply workgroup re-reading the
-        // 256 chunk partials cost more than the finalize launch: real Case4 at one
-        // chain 18.55 vs 18.71 ms per step, r05o)
-        // Also only with gn2's 256-thread layout (<= 64 chunks): config D's levels,
-        // not a small planned batch's 1024-thread chunks (Case4 at one chain: 96^2,
-        // 48^2), where the re-read partials cost more than the finalize launch
-        static const int gnb2 = getenv("CFD_GNB2") ? atoi(getenv("CFD_GNB2")) : 1;
+        // finalised inside the apply pass (config-D input-VJP -0.1-0.2 ms), with
+        // gn2's 256-thread layout (<= 64 chunks: config D's levels).  A small
+        // planned batch's 1024-thread chunks (Case4 at one chain: 96^2, 48^2) keep
+        // the finalize launch: every apply workgroup re-reading the 256 chunk
+        // partials cost more than it (real Case4 18.71 vs 18.55 ms per step, r05o)
         const int nc2 = gn2_chunks(a.HW, a.plan_b);
-        if (gnb2 == 2 || (gnb2 && gn2_threads(nc2) == 256)) {
+        if (gn2_threads(nc2) == 256) {
             a.nchunks = nc2;
             a.B = B;
             const dim3 grid((unsigned)a.nchunks, (unsigned)B);
-            if (gn2_threads(a.nchunks) == 1024) {
-                hipLaunchKernelGGL((gn_bwd_partial_kernel<false, 1024>), grid, dim3(1024), 0, st, a);
-                check_launch("gn_bwd_partial_kernel");
-                hipLaunchKernelGGL(gn_bwd_apply2_kernel<1024>, grid, dim3(1024), 0, st, a);
-            } else {
-                hipLaunchKernelGGL((gn_bwd_partial_kernel<false, 256>), grid, dim3(256), 0, st, a);
-                check_launch("gn_bwd_partial_kernel");
-                hipLaunchKernelGGL(gn_bwd_apply2_kernel<256>, grid, dim3(256), 0, st, a);
-            }
+            hipLaunchKernelGGL((gn_bwd_partial_kernel<false, 256>), grid, dim3(256), 0, st, a);
+            check_launch("gn_bwd_partial_kernel");
+            hipLaunchKernelGGL(gn_bwd_apply2_kernel<256>, grid, dim3(256), 0, st, a);
             check_launch("gn_bwd_apply2_kernel");
             return a.nchunks;
         }
