@@ -70,20 +70,32 @@ METRIC = "generated fields/sec (256-step sample + CNF decode), Case4 latent, 1/2
 #   (kernel name, peak in algorithmic fp32 TFLOP/s, basis, committed PMC record)
 ROOFLINE = {
     "split_f16": ("siren_split32", F16_PEAK_TFLOPS / 3,
-                  "f16 dense MFMA peak / 3 (three f16 MFMAs per fp32 product)", "r04_siren_split32_pmc.json"),
+                  "f16 dense MFMA peak / 3 (three f16 MFMAs per fp32 product)", "r06c_pipe_pmc.json"),
     "f32": ("siren_fused", FMA_PEAK_TFLOPS, "fp32 MFMA peak", "r01_siren_pmc.json"),
 }
+PIPE_PMC_PAIRS = 8 * S * GRID ** 3     # the r06c record's decodes: config B's 512 latent rows x 64^3
+CLOCK_RECORD = "r06c_siren_clock.json"  # tools/dev/siren_clock.py: the decoder's in-kernel clock
 
 
-def measured_traffic(mode, latents, npts):
-    """Per-launch fabric bytes of the decoder kernel from the committed rocprofv3
-    PMC record (tools/pmc_traffic.py), scaled from its launch geometry to this one
-    (valid for the same SIREN widths)."""
-    kname, _, _, fname = ROOFLINE[mode]
+def _profile(fname):
     try:
-        rec = json.load(open(os.path.join(ROOT, "profiles", fname)))
+        return json.load(open(os.path.join(ROOT, "profiles", fname)))
     except (OSError, ValueError):
         return None
+
+
+def measured_traffic(mode, latents, npts, cus=None):
+    """Per-launch fabric bytes of the decoder kernel from the committed rocprofv3
+    PMC record, scaled from its launch geometry to this one (same SIREN widths).
+    split_f16: the HEAD record of the pipelined config-B bench (tools/pipe_pmc.py),
+    the dispatches on `cus` CUs (the side-by-side half, or the whole chip)."""
+    kname, _, _, fname = ROOFLINE[mode]
+    rec = _profile(fname)
+    if rec is None:
+        return None
+    if "decoder_dispatches" in rec:
+        ds = [d for d in rec["decoder_dispatches"] if cus is None or d["cus"] == cus] or rec["decoder_dispatches"]
+        return sum(d["traffic_bytes"] for d in ds) / len(ds) * (latents * npts) / PIPE_PMC_PAIRS
     launch = rec.get("launch", {})
     ref_pairs = launch.get("latents", 0) * launch.get("coords", 0)
     if not ref_pairs or f"{kname}<" not in rec.get("kernel", ""):
@@ -91,18 +103,27 @@ def measured_traffic(mode, latents, npts):
     return rec["traffic_bytes_per_launch"] * (latents * npts) / ref_pairs
 
 
-def measured_mfma_util(kname):
-    """Matrix-pipe busy fraction and held clock from the committed rocprofv3 record
-    (tools/gpujob_mfma_util.sh, tools/mfma_util.py)."""
-    try:
-        rec = json.load(open(os.path.join(ROOT, "profiles", "r04_mfma_util.json")))
-    except (OSError, ValueError):
+def measured_mfma_util(mode, cus=None):
+    """Matrix-pipe busy fraction of the decoder from the committed HEAD PMC record
+    (the dispatches on `cus` CUs), and its clock measured inside the kernel
+    (s_memtime / s_memrealtime, tools/dev/siren_clock.py) under the same condition."""
+    kname, _, _, fname = ROOFLINE[mode]
+    rec = _profile(fname)
+    if rec is None or "decoder_dispatches" not in rec:
         return None
-    for k, v in rec.items():
-        if k.startswith(f"cfd::{kname}<") and isinstance(v, dict):
-            return {"mfma_busy_frac": v["mfma_busy_frac"], "held_clock_ghz": v["held_clock_ghz"],
-                    "source": "profiles/r04_mfma_util.json"}
-    return None
+    ds = [d for d in rec["decoder_dispatches"] if cus is None or d["cus"] == cus] or rec["decoder_dispatches"]
+    out = {"mfma_busy_frac": sum(d["mfma_busy_frac"] for d in ds) / len(ds),
+           "valu_per_mfma": sum(d["valu_per_mfma"] for d in ds) / len(ds),
+           "clock_ghz_grbm": sum(d["clock_ghz_grbm"] for d in ds) / len(ds),
+           "source": f"profiles/{fname} (rocprofv3 --pmc passes of bench.py --steps 4, serialised dispatches)"}
+    clk = _profile(CLOCK_RECORD)
+    if clk:
+        cond = "whole" if cus == 256 or cus is None else "piped"
+        if cond in clk and clk[cond]:
+            out["clock_ghz_in_kernel"] = clk[cond]["clock_ghz_median"]
+            out["clock_condition"] = cond
+            out["clock_source"] = f"profiles/{CLOCK_RECORD}"
+    return out
 
 
 def siren_flops_per_pair(d, L, c, nh, H):
@@ -957,6 +978,7 @@ def main():
             workload = (f"config C (Case4 CNF-only): SIREN(3,384,3,15,384) decode of {C_LATENTS} latents x 2^22 "
                         f"uniform coords, coordinate-sharded")
         dshare = 1.0 if pipe is None else pipe.cu_share
+        dcus = None if pipe is None else pipe.cus[1]
         rec = {
             "metric": METRIC if args.config == "B" else
             "decoded fields/sec (CNF-only, 2^22 coords per field), Case4 CNF, 1/2/4/8 GPU",
@@ -976,8 +998,13 @@ def main():
                        else C_COORDS, "parallelism": par},
             "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)", "achieved": achieved,
                          "peak": peak, "peak_basis": peak_basis, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": measured_traffic(mode, rows_local, npts) if args.config == "B" else None,
-                         "flops_per_launch": flops, "launch_ms": dec_ms, "pmc": measured_mfma_util(kname),
+                         "traffic": measured_traffic(mode, rows_local, npts, dcus) if args.config == "B" else None,
+                         "traffic_source": f"profiles/{ROOFLINE[mode][3]}" if args.config == "B" else None,
+                         # fields written + coordinates and per-point bounds read + the split weight image
+                         "algorithmic_bytes": rows_local * npts * c["c"] * 4 + npts * (c["d"] + 2 * c["c"]) * 4
+                         + c["nh"] * c["H"] * c["H"] * 4,
+                         "flops_per_launch": flops, "launch_ms": dec_ms,
+                         "pmc": measured_mfma_util(mode, dcus) if args.config == "B" else None,
                          **({"peak_sustained": F16_SUSTAINED_TFLOPS / 3 * dshare,
                              "frac_sustained": achieved / (F16_SUSTAINED_TFLOPS / 3 * dshare),
                              "sustained_basis": "measured back-to-back f16 MFMA on random operands / 3 "
@@ -997,6 +1024,15 @@ def main():
         if strong is not None:
             rec["strong"] = strong
         if args.config == "B":
+            # the whole chip's rate: every algorithmic FLOP of a step (256 U-Net
+            # forwards + the decode of its samples) / (ms_per_step x the chip peak)
+            step_flops = count * UNET_FLOPS_PER_SAMPLE * 256 + flops
+            chip = step_flops / (elapsed / args.steps) / 1e12
+            rec["roofline"]["frac_chip"] = chip / (F16_PEAK_TFLOPS / 3)
+            rec["roofline_chip"] = {"bound": "mfma", "flops_per_step": step_flops, "achieved": chip,
+                                    "peak": F16_PEAK_TFLOPS / 3, "unit": "TFLOP/s", "frac": chip / (F16_PEAK_TFLOPS / 3),
+                                    "basis": "all algorithmic FLOP of a step (U-Net x 256 + decode) / ms_per_step, "
+                                             "against the whole chip's split-f16 peak (f16 dense / 3)"}
             uf = count * UNET_FLOPS_PER_SAMPLE * 256
             ua = uf / (unet_ms / 1e3) / 1e12
             # pipelined: all but the first batch sample on the other CU half
