@@ -74,7 +74,7 @@ ROOFLINE = {
     "f32": ("siren_fused", FMA_PEAK_TFLOPS, "fp32 MFMA peak", "r01_siren_pmc.json"),
 }
 PIPE_PMC_PAIRS = 8 * S * GRID ** 3     # the r06c record's decodes: config B's 512 latent rows x 64^3
-CLOCK_RECORD = "r06c_siren_clock.json"  # tools/dev/siren_clock.py: the decoder's in-kernel clock
+CLOCK_RECORD = "r06d_siren_clock.json"  # tools/dev/siren_clock.py: the decoder's in-kernel clock
 
 
 def _profile(fname):

@@ -1067,6 +1067,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
               if (a.kvf && !part) {
                 const int CH = a.kv_ch, C3 = 3 * CH, T = a.kv_T, nj = CH >> 5, nd = CH >> 4;
                 const float ks = kln2(a.kv_scale);
+                // head and sample of a (row, column): fdiv24 (exact below 2^24 pixels,
+                // launch_conv's bufaddr bound) instead of two integer divisions per
+                // item, which were most of this epilogue's VALU
+                const float rc3 = 1.0f / (float)C3, rT = 1.0f / (float)T;
+                const bool small = a.M < (1 << 24);
                 h8v* kf = (h8v*)a.kvf;
                 h8v* vf = kf + a.kv_voff;
                 const int mband = m0 + band * RB;
@@ -1075,9 +1080,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                     const int row = it / (BN / 8), c8 = (it - row * (BN / 8)) * 8;
                     const int m = mband + row, n = n0 + c8;
                     if (m >= a.M || n >= a.Cout) continue;
-                    const int hh = n / C3, o = n - hh * C3;
+                    const int hh = small ? fdiv24(n, C3, rc3) : n / C3, o = n - hh * C3;
                     if (o < CH || o >= 2 * CH) continue;
-                    const int kc = o - CH, b = m / T, key = m - b * T;
+                    const int b = small ? fdiv24(m, T, rT) : m / T;
+                    const int kc = o - CH, key = m - b * T;
                     f4 v0 = *(const f4*)&tile[sw(row, c8)], v1 = *(const f4*)&tile[sw(row, c8 + 4)];
                     v0 = v0 + *(const f4*)(a.bias + n);
                     v1 = v1 + *(const f4*)(a.bias + n + 4);
@@ -1099,9 +1105,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_gemm_kernel(Con
                     const int col = it % BN, r2 = it / BN, g = r2 & 3, blk = r2 >> 2;
                     const int n = n0 + col, mb = mband + 32 * blk;
                     if (n >= a.Cout || mb >= a.M) continue;
-                    const int hh = n / C3, o = n - hh * C3;
+                    const int hh = small ? fdiv24(n, C3, rc3) : n / C3, o = n - hh * C3;
                     if (o < 2 * CH) continue;
-                    const int vc = o - 2 * CH, b = mb / T, kb = (mb - b * T) >> 5;
+                    const int b = small ? fdiv24(mb, T, rT) : mb / T;
+                    const int vc = o - 2 * CH, kb = (mb - b * T) >> 5;
                     const float bn = a.bias[n];
                     float v[8];
 #pragma unroll

@@ -4,6 +4,8 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r06d; mkdir -p $O
+timeout -k 10 600 python3 tools/libdiff.py libconfild_hip_pre.so libconfild_hip.so > $O/libdiff.json 2> $O/libdiff.err || { cat $O/libdiff.json; tail -20 $O/libdiff.err; exit 9; }
+cat $O/libdiff.json
 CFD_LIB=libconfild_hip_stamps.so timeout -k 10 300 python3 tools/dev/siren_clock.py --json $O/siren_clock.json > $O/siren_clock.log 2>&1 || { tail -20 $O/siren_clock.log; exit 1; }
 python3 -c "import json; d=json.load(open('$O/siren_clock.json')); print({k: (v['clock_ghz_median'], v['launch_ms']) for k, v in d.items() if isinstance(v, dict)}, d['piped'].get('decode_within_sampling'))"
 run_trace() {  # name, per, command...
