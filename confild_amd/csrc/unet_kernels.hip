@@ -1813,6 +1813,20 @@ void launch_gn(const GnArgs& a0, int B, hipStream_t st) {
     const int ipt = gn_reg_ipt(a);
     if (ipt > 0 && ipt <= 32) {
         const dim3 grid((unsigned)(32 * B));
+        // small groups (<= 1024 float4 per (sample, group): the 16^2 / 8^2 levels):
+        // 256-thread workgroups, up to 4 float4 per thread -- a quarter of the waves
+        // to gather at the statistics barrier
+        const int nq = a.Ctot / 128, r256 = 256 / nq, i256 = (a.HW + r256 - 1) / r256;
+        if (i256 <= 4) {
+            if (i256 <= 1)
+                hipLaunchKernelGGL((gn_fused_reg_kernel<1, 256>), grid, dim3(256), 0, st, a);
+            else if (i256 <= 2)
+                hipLaunchKernelGGL((gn_fused_reg_kernel<2, 256>), grid, dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((gn_fused_reg_kernel<4, 256>), grid, dim3(256), 0, st, a);
+            check_launch("gn_fused_reg_kernel");
+            return;
+        }
         if (ipt <= 4)
             hipLaunchKernelGGL((gn_fused_reg_kernel<2, 1024>), grid, dim3(1024), 0, st, a);
         else if (ipt <= 8)
@@ -1945,24 +1959,25 @@ int smalln_below() {
 
 template <bool TMODE, int MODE, bool BUFA>
 static void launch_conv_tiles_(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-    if constexpr (!TMODE && MODE == 2 && BUFA) {   // the split-f16 forward
-        // small batch: where the 128 x 128 grid leaves most CUs idle (< 128
+    if constexpr (MODE != 0 && BUFA) {   // the split-f16 / bf16 tiles, forward and transposed
+        // small batch (forward): where the 128 x 128 grid leaves most CUs idle (< 128
         // workgroups of 8 waves, two per SIMD), 128 x 64 tiles of 8 waves (32 x 32
         // each) -- twice the workgroups, half the work per wave, the same tiles'
         // sums (CFD_CONV_SMALLN=0 keeps 128 x 128)
         static const int smalln = smalln_below();
-        if (p.nw == 8 && p.bm == 128 && p.bn == 128 && (int64_t)grid.x * grid.y * grid.z < smalln &&
+        if (!TMODE && p.nw == 8 && p.bm == 128 && p.bn == 128 && (int64_t)grid.x * grid.y * grid.z < smalln &&
             a.Cout % 64 == 0) {
             const dim3 g64(grid.x, (unsigned)ceil_div(a.Cout, 64), grid.z);
-            hipLaunchKernelGGL((conv_gemm_kernel<128, 64, false, 2, 8, true>), g64, dim3(512), 0, st, a);
+            hipLaunchKernelGGL((conv_gemm_kernel<128, 64, false, MODE, 8, true>), g64, dim3(512), 0, st, a);
             return;
         }
+        // the register ring of K tiles (p.pf deep; the same tiles in the same order)
         if (p.nw == 8 && p.bm == 128 && p.bn == 128 && p.pf == 2) {
-            hipLaunchKernelGGL((conv_gemm_kernel<128, 128, false, 2, 8, true, 2>), grid, dim3(512), 0, st, a);
+            hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE, 8, true, 2>), grid, dim3(512), 0, st, a);
             return;
         }
         if (p.nw == 8 && p.bm == 128 && p.bn == 128 && p.pf == 3) {
-            hipLaunchKernelGGL((conv_gemm_kernel<128, 128, false, 2, 8, true, 3>), grid, dim3(512), 0, st, a);
+            hipLaunchKernelGGL((conv_gemm_kernel<128, 128, TMODE, MODE, 8, true, 3>), grid, dim3(512), 0, st, a);
             return;
         }
     }
