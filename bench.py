@@ -285,62 +285,128 @@ class PipelineB:
     batch k is sampled on the other; the first batch samples on the whole chip.
     Every batch is sampled and decoded exactly once inside the timed region (no
     work moves out of it); only the order of independent batches overlaps.
-    Measured (tools/dev/cu_split_probe.py, one box): sampling 1.03 s + decode
-    1.35 s in sequence = 2.38 s per batch; side by side on 128 + 128 CUs 2.17 s."""
 
-    def __init__(self, o, dev, start, count, sizes, world, gather):
+    The sampler finishes its batch first (round 5: 1.6 s against the decode's
+    2.2 s per batch on 128 + 128 CUs), so the decode of batch k-1 is split by
+    latent rows: rows [0, n1) on the decode half beside the sampling, rows
+    [n1, R) on the sampling half right after it, written into one (R, N, c)
+    tensor.  n1 is re-balanced from the measured rates of the batch before last
+    so that both halves finish together.  A row's fields are the same bits
+    whichever launch decodes it (one workgroup = one latent row x 128 coordinates;
+    tests/test_gpu_pipeline.py)."""
+
+    def __init__(self, o, dev, start, count, sizes, world, gather, sample_cus=None, split=True):
         from confild_amd.streams import CuRangeStream, cu_count
         n = cu_count(dev)
-        h = int(os.environ.get("CFD_PIPE_SAMPLE_CUS", n // 2))   # CUs of the sampling half (development)
+        h = n // 2 if sample_cus is None else int(sample_cus)   # CUs of the sampling half
         self.su = CuRangeStream(dev, 0, h)
         self.sd = CuRangeStream(dev, h, n - h)
         self.cus = (h, n - h)
         self.cu_share = (n - h) / n
         self.o, self.dev, self.start, self.count = o, dev, start, count
         self.sizes, self.world, self.gather = sizes, world, gather
+        self.R = count * S
+        self.split = split
+        self.n1 = self.R if not split else self._rows(0.86 * self.R)
+        self.hist = []        # per side-by-side batch: (sampling events, part-B events, n1, part-A events)
+        # the gather of a finished batch waits for both halves' parts on a stream of
+        # its own (an unmasked, non-default stream), so neither half waits for the other
+        self.sg = torch.cuda.Stream(dev) if gather else None
 
-    def _decode(self, den, ready, evd, stream=None):
-        # nothing is enqueued on the default stream between the first sample and the
-        # end: it is the legacy NULL stream, and any operation on it orders every
-        # blocking stream behind it (a wait there serialised the two halves)
-        sd = self.sd.stream if stream is None else stream
-        sd.wait_event(ready)
-        with torch.cuda.stream(sd):
-            d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            d0.record()
-            f = self.o["nf"].decode(self.o["coords"], den.reshape(self.count * S, 1, S), self.o["xn"], self.o["yn"])
-            d1.record()
-            f = gather_to_root(f, 0, self.sizes, self.world) if self.gather else f   # RCCL on this stream
-        den.record_stream(sd)
-        evd.append((d0, d1))
+    def _rows(self, x):
+        return int(max(self.R // 2, min(self.R, round(x / 8) * 8)))
+
+    def _rebalance(self):
+        """n1 for the next batch from a finished one: the rows the decode half
+        covers in the time the sampling half takes to sample and decode the rest."""
+        if len(self.hist) < 2:
+            return
+        (u0, u1), (d0, d1), n1, pa = self.hist[-2]
+        if pa is None or not all(e.query() for e in (u1, d1, pa[1])):
+            return
+        ts, tb, ta = u0.elapsed_time(u1), d0.elapsed_time(d1), pa[0].elapsed_time(pa[1])
+        n2 = self.R - n1
+        if tb <= 0 or ta <= 0 or n2 <= 0:
+            return
+        rb, ra = n1 / tb, n2 / ta
+        self.n1 = self._rows((ts + self.R / ra) / (1 / rb + 1 / ra))
+
+    def _decode_rows(self, den, full, r0, r1, stream):
+        with torch.cuda.stream(stream):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.o["nf"].decode(self.o["coords"], den.reshape(self.R, 1, S)[r0:r1], self.o["xn"], self.o["yn"],
+                                out=full[r0:r1])
+            e1.record()
+        den.record_stream(stream)
+        return e0, e1
+
+    def _finish(self, full, events):
+        """The gather of a batch once every part of it is written (multi-GPU)."""
+        if not self.gather:
+            return full
+        for e in events:
+            self.sg.wait_event(e)
+        with torch.cuda.stream(self.sg):
+            f = gather_to_root(full, 0, self.sizes, self.world)   # RCCL on the gather stream
         return f
 
     def run(self, seeds, keep=None):
         """Samples and decodes one batch per seed; returns (sampling events,
-        the side-by-side decodes' events, the last batch's fields).  `keep` (a
-        list, tests): every batch's fields are appended to it in seed order."""
+        the side-by-side decode-half parts' events, the last batch's fields).
+        `keep` (a list, tests): every batch's fields are appended to it in seed
+        order.  self.rows_b: the rows of each side-by-side decode-half part."""
+        # nothing is enqueued on the default stream between the first sample and the
+        # end: it is the legacy NULL stream, and any operation on it orders every
+        # blocking stream behind it (a wait there serialised the two halves)
         main = torch.cuda.current_stream(self.dev)
+        nf, coords = self.o["nf"], self.o["coords"]
         evu, evd, pend, out = [], [], None, None
+        self.rows_b = []
+        # every batch's field tensor stays referenced until the run has ended (the
+        # two halves write its parts; main waits for both before returning), so
+        # no block is re-used while a part is still being written -- and none is
+        # tied to the CU-masked streams, which close() destroys
+        self._live = []
         for i, seed in enumerate(seeds):
             if pend is not None:
-                out = self._decode(pend[0], pend[1], evd)
-                if keep is not None:
-                    keep.append(out)
-                self.su.stream.wait_event(pend[1])   # the sampler's buffers: one batch at a time
+                den, ready = pend
+                full = torch.empty((self.R, coords.shape[0], nf.out_features), dtype=torch.float32, device=self.dev)
+                self._live.append(full)
+                n1 = self.n1
+                self.sd.stream.wait_event(ready)
+                eb = self._decode_rows(den, full, 0, n1, self.sd.stream)
+                evd.append(eb)
+                self.rows_b.append(n1)
+                self.su.stream.wait_event(ready)   # the sampler's buffers: one batch at a time
             with torch.cuda.stream(main if i == 0 else self.su.stream):
                 u0, u1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 u0.record()
-                den = sample_B(self.o, self.dev, seed, self.start, self.count)
+                den_next = sample_B(self.o, self.dev, seed, self.start, self.count)
                 u1.record()
             evu.append((u0, u1))
-            pend = (den, u1)
+            if pend is not None:
+                ea = self._decode_rows(den, full, n1, self.R, self.su.stream) if n1 < self.R else None
+                self.hist.append(((u0, u1), eb, n1, ea))
+                out = self._finish(full, [eb[1]] + ([ea[1]] if ea else []))
+                if keep is not None:
+                    keep.append(out)
+                if self.split:
+                    self._rebalance()
+            pend = (den_next, u1)
         # the last batch: its decode on the whole chip once both halves are done
         main.wait_stream(self.su.stream)
         main.wait_stream(self.sd.stream)
-        evl = []
-        out = self._decode(pend[0], pend[1], evl, stream=main)
+        if self.sg is not None:
+            main.wait_stream(self.sg)
+        den, ready = pend
+        full = torch.empty((self.R, coords.shape[0], nf.out_features), dtype=torch.float32, device=self.dev)
+        with torch.cuda.stream(main):
+            nf.decode(coords, den.reshape(self.R, 1, S), self.o["xn"], self.o["yn"], out=full)
+            out = gather_to_root(full, 0, self.sizes, self.world) if self.gather else full
         if keep is not None:
             keep.append(out)
+        self._live = [] if keep is None else self._live   # main has waited for both halves
         return evu, evd, out
 
     def close(self):
@@ -943,7 +1009,9 @@ def main():
         barrier(dev, world)
         elapsed = max_over_ranks(time.perf_counter() - t0, dev, world)
         unet_ms = float(np.mean([a.elapsed_time(b) for a, b in evu]))
-        dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evd]))   # the side-by-side decodes (half chip)
+        # the decode half's side-by-side parts (rows [0, n1) of each batch)
+        dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evd]))
+        dec_rows = float(np.mean(pipe.rows_b))
         peak, peak_basis = peak * pipe.cu_share, f"{peak_basis} x the decode stream's CU share {pipe.cu_share:g}"
     else:
         for w in range(args.warmup):
@@ -958,7 +1026,10 @@ def main():
         unet_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in evs]))
         dec_ms = float(np.mean([ev[1].elapsed_time(ev[2]) for ev in evs]))
     value = fields_per_step * args.steps / elapsed
-    flops = rows_local * npts * siren_flops_per_pair(**c)
+    # FLOP of one timed decoder launch: a whole batch's rows, or (pipelined) the
+    # decode half's part of a batch
+    launch_rows = rows_local if pipe is None else dec_rows
+    flops = launch_rows * npts * siren_flops_per_pair(**c)
     achieved = flops / (dec_ms / 1e3) / 1e12
     if rank == 0 and out is not None:
         assert torch.isfinite(out).all().item(), "non-finite output"
@@ -998,12 +1069,12 @@ def main():
                        else C_COORDS, "parallelism": par},
             "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)", "achieved": achieved,
                          "peak": peak, "peak_basis": peak_basis, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": measured_traffic(mode, rows_local, npts, dcus) if args.config == "B" else None,
+                         "traffic": measured_traffic(mode, launch_rows, npts, dcus) if args.config == "B" else None,
                          "traffic_source": f"profiles/{ROOFLINE[mode][3]}" if args.config == "B" else None,
                          # fields written + coordinates and per-point bounds read + the split weight image
-                         "algorithmic_bytes": rows_local * npts * c["c"] * 4 + npts * (c["d"] + 2 * c["c"]) * 4
+                         "algorithmic_bytes": launch_rows * npts * c["c"] * 4 + npts * (c["d"] + 2 * c["c"]) * 4
                          + c["nh"] * c["H"] * c["H"] * 4,
-                         "flops_per_launch": flops, "launch_ms": dec_ms,
+                         "flops_per_launch": flops, "launch_ms": dec_ms, "launch_rows": launch_rows,
                          "pmc": measured_mfma_util(mode, dcus) if args.config == "B" else None,
                          **({"peak_sustained": F16_SUSTAINED_TFLOPS / 3 * dshare,
                              "frac_sustained": achieved / (F16_SUSTAINED_TFLOPS / 3 * dshare),
@@ -1017,16 +1088,19 @@ def main():
             rec["plan_batch"] = o["model"].plan_batch or B
         if pipe is not None:
             rec["pipeline"] = {"sample_cus": pipe.cus[0], "decode_cus": pipe.cus[1],
-                               "sample_ms_per_batch": unet_ms, "decode_ms_per_batch": dec_ms,
-                               "note": "batch k-1 decoded on one CU half while batch k samples on the other; "
-                                       "the first batch samples and the last decodes on the whole chip "
-                                       "(bench.py PipelineB); roofline.launch_ms = the side-by-side decodes"}
+                               "sample_ms_per_batch": unet_ms, "decode_half_ms_per_batch": dec_ms,
+                               "rows_per_batch": pipe.R, "decode_half_rows": pipe.rows_b,
+                               "note": "batch k-1 decoded while batch k samples: rows [0, n1) on the decode CU "
+                                       "half beside the sampling, rows [n1, R) on the sampling half after it "
+                                       "(n1 re-balanced per batch); the first batch samples and the last decodes "
+                                       "on the whole chip (bench.py PipelineB); roofline.launch_ms and "
+                                       "flops_per_launch = the decode half's parts"}
         if strong is not None:
             rec["strong"] = strong
         if args.config == "B":
             # the whole chip's rate: every algorithmic FLOP of a step (256 U-Net
             # forwards + the decode of its samples) / (ms_per_step x the chip peak)
-            step_flops = count * UNET_FLOPS_PER_SAMPLE * 256 + flops
+            step_flops = count * UNET_FLOPS_PER_SAMPLE * 256 + rows_local * npts * siren_flops_per_pair(**c)
             chip = step_flops / (elapsed / args.steps) / 1e12
             rec["roofline"]["frac_chip"] = chip / (F16_PEAK_TFLOPS / 3)
             rec["roofline_chip"] = {"bound": "mfma", "flops_per_step": step_flops, "achieved": chip,

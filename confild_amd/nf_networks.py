@@ -199,9 +199,11 @@ class SIRENAutodecoder_film(nn.Module):
                 ymin = ymin.reshape(-1).contiguous()
         return cf, xmax, xmin, ymax, ymin, ystride, post
 
-    def decode(self, coords, latents, x_normalizer=None, y_normalizer=None):
+    def decode(self, coords, latents, x_normalizer=None, y_normalizer=None, out=None):
         """denorm(NF(norm(coords), latents)) in one fused launch (trainer.infer,
-        N/scripts/train.py:265-279; pass_through_model_batch, inference_function.py:22-48)."""
+        N/scripts/train.py:265-279; pass_through_model_batch, inference_function.py:22-48).
+        ``out``: a contiguous fp32 (b, N, c) tensor the fields are written into (e.g.
+        a row slice of a larger batch; fused '-11' output normalisers only)."""
         d, L, c = self.in_coord_features, self.in_latent_features, self.out_features
         dev = latents.device
         if dev.type != "cuda":
@@ -220,7 +222,12 @@ class SIRENAutodecoder_film(nn.Module):
         lib = _lib.load()
         _lib.check(lib.cfd_siren_workspace_bytes(h, b, C.byref(nbytes)), "siren workspace")
         ws = torch.empty(max(nbytes.value, 16), dtype=torch.uint8, device=dev)
-        out = torch.empty((b, N, c), dtype=torch.float32, device=dev)
+        if out is None:
+            out = torch.empty((b, N, c), dtype=torch.float32, device=dev)
+        elif (tuple(out.shape) != (b, N, c) or out.dtype != torch.float32 or not out.is_contiguous()
+              or out.device != dev or post is not None):
+            raise ValueError(f"out must be a contiguous fp32 ({b}, {N}, {c}) tensor on {dev} (fused '-11' output "
+                             f"normaliser only)")
         _lib.check(lib.cfd_siren_forward(h, _lib.ptr(cf), N, _lib.ptr(lat), b, _lib.ptr(xmax), _lib.ptr(xmin),
                                          _lib.ptr(ymax), _lib.ptr(ymin), ystride, _lib.ptr(out), _lib.ptr(ws),
                                          ws.numel(), _lib.stream_of(dev)), "cfd_siren_forward")

@@ -51,6 +51,9 @@ class CuRangeStream:
         return False
 
     def __del__(self):
+        import sys
+        if sys.is_finalizing():   # the HIP runtime may already be gone
+            return
         try:
             self.close()
         except Exception:

@@ -2,9 +2,12 @@
 as a two-stage pipeline over the chip's CU halves: the decode of batch k-1 on
 one half while batch k samples on the other, cross-stream events between them)
 must give, for every batch, the same bits as step_B -- the same seed sampled
-and decoded in sequence on the whole chip.  An ordering bug between the two
-streams (a decode reading a latent the sampler is still writing, a sampler
-overwriting the buffers of a pending decode) would show here as a mismatch.
+and decoded in sequence on the whole chip.  Each side-by-side decode is split by
+latent rows between the decode half (beside the sampling) and the sampling half
+(after it), re-balanced per batch; the rows' fields must not depend on the
+split.  An ordering bug between the two streams (a decode reading a latent the
+sampler is still writing, a sampler overwriting the buffers of a pending
+decode) would show here as a mismatch.
 
 The second test runs the pipelined decode's RCCL gather (dist.gather on the
 CU-masked decode stream, bench.py gather_to_root) under a one-rank "nccl"
@@ -40,6 +43,9 @@ def test_pipeline_fields_equal_sequential_step(cfgB):
     torch.cuda.synchronize()
     assert len(kept) == len(seeds) and kept[-1] is last
     assert len(evu) == len(seeds) and len(evd) == len(seeds) - 1
+    # the side-by-side decodes were split by rows between the two CU halves
+    assert len(pp.rows_b) == len(seeds) - 1 and pp.rows_b[0] < COUNT * bench.S
+    assert all(COUNT * bench.S // 2 <= r <= COUNT * bench.S for r in pp.rows_b)
     for seed, f in zip(seeds, kept):
         ref = bench.step_B(o, DEV, seed, 0, COUNT)
         torch.cuda.synchronize()
