@@ -563,27 +563,7 @@ static void launch_tn(const float* X, int64_t ldx, const float* Y, int64_t ldy, 
 //   siren_latent_grad  g_z[r] = sum_i V_i^T (sum_s delta_i[r, s]) in a fixed order
 //                   (deterministic, batch invariant).
 // ---------------------------------------------------------------------------
-struct SirenTapeArgs {
-    const float* w0;      // (H, d)
-    const float* wimg;    // forward weight image (as SirenArgs)
-    const float* wimg_t;  // transposed image, layers nh..1: img[j][q][lane][s] = W_i[16q+4g+s][16j+(lane&15)]
-    const float* wout;    // (c, H)
-    const float* bout;    // (c)
-    const float* film;    // (R, nh+1, H)
-    const float* coords;  // (Ns, d)
-    const float* xmax;
-    const float* xmin;
-    const float* ymax;
-    const float* ymin;
-    float* u;             // (P, nh+1, H) tape
-    float* delta;         // (P, nh+1, H)
-    float* out;           // (P, c)
-    const float* gout;    // (P, c)
-    int64_t P;
-    int64_t ystride;
-    int Ns, d, c, nh;
-    float w0f;
-};
+// (SirenTapeArgs: siren.hpp)
 
 template <int NB, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void siren_tape_fwd(SirenTapeArgs p) {
@@ -1081,6 +1061,7 @@ struct cfd_siren {
     float* bout = nullptr;  // (c)
     float* wimg_t = nullptr; // transposed weight image, layers nh..1 (latent-gradient path)
     float* wimg16 = nullptr; // split-f16 image (hi, lo) of the scaled hidden weights, same bytes as wimg
+    float* wimg16t = nullptr; // the same image of the transposes, layers nh..1 (K9t backward)
     float* wscale = nullptr; // (nh) power-of-two scale of each hidden layer in wimg16
     float* wimg32 = nullptr; // the same split in the 32x32x16 chain's k order (siren_split32)
     float* wimg32r = nullptr; // siren_split32 image of W (w0 / 2pi) s'_i: accumulators in revolutions
@@ -1155,6 +1136,20 @@ void pack_split_f16(cfd_siren* h, int li, const float* W) {
                 }
     CFD_HIP(hipMemcpy(h->wimg16 + (size_t)(li - 1) * NB * NB * 256, img.data(), img.size() * sizeof(_Float16),
                       hipMemcpyHostToDevice));
+    // the same image of W^T (same scale), at slot nh - li: the K9t backward's A operand
+    for (int j = 0; j < NB; ++j)
+        for (int q = 0; q < NQ; ++q)
+            for (int l = 0; l < 64; ++l)
+                for (int t = 0; t < 8; ++t) {
+                    const float v = W[(size_t)(16 * (2 * q + t / 4) + 4 * (l / 16) + t % 4) * H + 16 * j + l % 16] * s;
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    const size_t base = ((size_t)j * NB + 2 * q) * 512 + l * 8 + t;
+                    img[base] = hi;
+                    img[base + 512] = lo;
+                }
+    CFD_HIP(hipMemcpy(h->wimg16t + (size_t)(h->cfg.num_hidden_layers - li) * NB * NB * 256, img.data(),
+                      img.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     // 32x32x16 image: block J (32 rows), K-chunk k = 2 jb + e: 1 KiB of Wh then
     // 1 KiB of Wl, lane-linear, lane l element t =
     // W[32J + l%32][32 jb + 8(2e + t/4) + 4(l/32) + t%4]
@@ -1243,6 +1238,7 @@ extern "C" int cfd_siren_create(const cfd_siren_cfg* cfg, int device, cfd_siren*
         CFD_HIP(hipMalloc(&h->bout, sizeof(float) * 4));
         CFD_HIP(hipMalloc(&h->wimg_t, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wimg16, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
+        CFD_HIP(hipMalloc(&h->wimg16t, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wscale, sizeof(float) * (size_t)std::max(nh, 1)));
         CFD_HIP(hipMalloc(&h->wimg32, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
         CFD_HIP(hipMalloc(&h->wimg32r, sizeof(float) * (size_t)std::max(nh, 1) * NB * NB * 256));
@@ -1261,6 +1257,7 @@ extern "C" void cfd_siren_destroy(cfd_siren* h) {
     (void)hipFree(h->bout);
     (void)hipFree(h->wimg_t);
     (void)hipFree(h->wimg16);
+    (void)hipFree(h->wimg16t);
     (void)hipFree(h->wscale);
     (void)hipFree(h->wimg32);
     (void)hipFree(h->wimg32r);
@@ -1453,6 +1450,12 @@ void tape_args(const cfd_siren* h, cfd::SirenTapeArgs& a, int64_t Ns, int R, voi
     a.c = h->cfg.out_features;
     a.nh = nh;
     a.w0f = h->cfg.w0;
+    // K9t (split-f16 tape) in split compute for the widths it has a form for
+    if (h->compute == CFD_SIREN_SPLIT_F16 && nh >= 1 && cfd::tape_split_supported(h->NB)) {
+        a.wimg16 = h->wimg16;
+        a.wimg16t = h->wimg16t;
+        a.wscale = h->wscale;
+    }
 }
 
 // waves per workgroup: 4 when there are enough pairs to fill the chip, else fewer
@@ -1487,9 +1490,13 @@ void launch_tape_ks(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
 
 template <int NB>
 void launch_tape_nb(const cfd::SirenTapeArgs& a, bool bwd, hipStream_t st) {
-    // K-split tiles where one wave per 16 pairs leaves most SIMDs idle
+    // K-split tiles where one wave per 16 pairs leaves most SIMDs idle: K9t in
+    // split compute (tape_args set its images), else the fp32 MFMA form
     if constexpr (NB % 4 == 0 && NB <= 24) {
-        if (a.P < 16 * 2048) return launch_tape_ks<NB, 4>(a, bwd, st);
+        if (a.P < 16 * 2048) {
+            if (a.wimg16) return cfd::launch_tape_split(NB, a, bwd, st);
+            return launch_tape_ks<NB, 4>(a, bwd, st);
+        }
     }
     switch (tape_waves(a.P)) {
         case 4: return launch_tape_w<NB, 4>(a, bwd, st);

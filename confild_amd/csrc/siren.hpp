@@ -41,6 +41,32 @@ struct SirenArgs {
     float w0f;
     unsigned long long* stamps;   // development (CFD_STAMPS builds): timestamp buffer, else null
 };
+// Tape kernels of the DPS adjoint and the CNF training backward (siren.hip):
+// pre-activations u and deltas of every layer for P = R x Ns (row, sensor) pairs
+struct SirenTapeArgs {
+    const float* w0;      // (H, d)
+    const float* wimg;    // forward weight image (as SirenArgs)
+    const float* wimg_t;  // transposed image, layers nh..1: img[j][q][lane][s] = W_i[16q+4g+s][16j+(lane&15)]
+    const float* wout;    // (c, H)
+    const float* bout;    // (c)
+    const float* film;    // (R, nh+1, H)
+    const float* coords;  // (Ns, d)
+    const float* xmax;
+    const float* xmin;
+    const float* ymax;
+    const float* ymin;
+    float* u;             // (P, nh+1, H) tape
+    float* delta;         // (P, nh+1, H)
+    float* out;           // (P, c)
+    const float* gout;    // (P, c)
+    const float* wimg16;  // split-f16 image of the hidden weights (pack_split_f16), null: fp32 tape
+    const float* wimg16t; // split-f16 image of their transposes, layers nh..1 (pack_split_f16t)
+    const float* wscale;  // (nh) the power-of-two scale of both images
+    int64_t P;
+    int64_t ystride;
+    int Ns, d, c, nh;
+    float w0f;
+};
 // the CFD_STAMPS build's timestamp buffer (unet_kernels.hip; null: off)
 unsigned long long* stamps_buf();
 
@@ -60,11 +86,32 @@ __device__ __forceinline__ void siren_issue_block(const float* __restrict__ wimg
     }
 }
 
+// The same with the piece loop unrolled (NB % WAVES == 0: NB / WAVES pieces per
+// wave, a compile-time count, so the compiler's vmcnt accounting stays exact
+// across the issue instead of falling back to vmcnt(0) at the next use of an
+// earlier load)
+template <int NB, int WAVES>
+__device__ __forceinline__ void siren_issue_block_u(const float* __restrict__ wimg, int J, float* dst,
+                                                    int wave, int lane) {
+    static_assert(NB % WAVES == 0, "whole pieces per wave");
+    constexpr int BLK = NB * 256;
+    const float* src = wimg + (int64_t)__builtin_amdgcn_readfirstlane(J) * BLK;
+    static_for<NB / WAVES>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        const int piece = wave + m * WAVES;
+        __builtin_amdgcn_global_load_lds((const void*)(src + piece * 256 + lane * 4),
+                                         (__attribute__((address_space(3))) void*)(dst + piece * 256), 16, 0, 0);
+    });
+}
+
 // Split-f16 chain (siren_split.hip).  Defined for even NB (H a multiple of 32).
 bool siren_split_supported(int NB);
 void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st);
 // 32x32x16 form of the chain (K7t, image from pack_split_f16_32)
 bool siren_split32_supported(int H, int nh);
 void launch_siren_split32(int H, SirenArgs a, int b, hipStream_t st);
+// split-f16 K-split tape kernels (K9t, siren_split.hip): null when NB has no form
+bool tape_split_supported(int NB);
+void launch_tape_split(int NB, const SirenTapeArgs& a, bool bwd, hipStream_t st);
 
 }  // namespace cfd

@@ -166,6 +166,8 @@ __device__ __forceinline__ f2 sin2_sel(f2 x) {
 
 // s_waitcnt immediate waiting for vmcnt <= n only (expcnt, lgkmcnt at their maxima)
 constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
+// the same with lgkmcnt 0 (the wave's LDS accesses retired too)
+constexpr int vm_lgkm0_imm(int n) { return vmcnt_imm(n) & ~(15 << 8); }
 
 // CG column groups of 16 coordinates per wave share every A-fragment read (CG = 2:
 // one wave per SIMD, 512 registers; CG = 1: two waves per SIMD, 256 registers).
@@ -798,6 +800,413 @@ void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st) {
         case 16: return launch_nb<16>(a, b, st);
         case 24: return launch_nb<24>(a, b, st);
         default: throw Error{CFD_EARG, "split-f16 SIREN needs hidden_features = 32*{1,2,3,4,6,8,12,16}"};
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K9t: the tape kernels of the DPS adjoint on split-f16 MFMA (the K-split forms
+// of siren_tape_fwd_ks / siren_tape_bwd_ks, siren.hip, with every hidden-layer
+// product W x as three v_mfma_f32_16x16x32_f16 on hi/lo halves, K7s's scheme).
+// KS waves share one 16-pair tile; wave w owns output blocks [QW w, QW (w + 1))
+// and holds exactly those features as its next-layer operand: QW / 2 K-chunks of
+// 32 features in the accumulator-as-B k order of pack_split_f16, split once per
+// layer.  Per output block every wave multiplies its chunks by the block's
+// weights (one block per ring slot, LDS-DMA, fetched one block ahead) and parks
+// the partial in LDS.  The epilogue of block j -- the KS partials added in wave
+// order (fixed: deterministic, batch invariant), the weight scale undone, the
+// FiLM row added, the sine / the cos derivative -- runs in block j + 1 between
+// that block's MFMAs (every wave computes it, pinned there; the owner keeps it
+// and stores the tape), the FiLM rows / pre-activations of a wave's own blocks
+// are loaded once per layer, and each block ends on a bare s_barrier after
+// vmcnt(1) -- the tape store stays in flight (memory operations retire in order)
+// where __syncthreads' fence would wait for it.
+// Operand range: the forward's operands are sines (|x| <= 1).  The backward's
+// deltas have no bound, so each wave scales its slice of a pair's deltas by a
+// power of two 2^-e (e: exponent of the slice's max |delta|, per pair and per
+// wave: a pair's bits never depend on its tile neighbours) before the split and
+// multiplies its partial by 2^e -- exact -- so the f16 halves keep 22 bits
+// whatever the gradient's scale.
+// Lanes past the last pair compute pair P - 1 again (same inputs, same bits), so
+// every tape store is issued by every lane and the vmcnt accounting is exact.
+// ---------------------------------------------------------------------------
+template <int NB, int KS>
+__global__ __launch_bounds__(64 * KS) void siren_tape_fwd_split(SirenTapeArgs p) {
+    constexpr int H = NB * 16, BLK = NB * 256, QW = NB / KS, QC = QW / 2;
+    static_assert(QW % 2 == 0, "K9t: an even block count per wave");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* wbuf = smem;                  // 2 ring slots
+    float* w0s = smem + 2 * BLK;         // (H, 4)
+    float* red = w0s + 4 * H;            // 2 x KS x 64 lanes x f4 partial sums
+    float* osum = red + 2 * KS * 256;    // KS x 4 x 16
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int64_t row = nc / p.Ns;
+    const int sensor = (int)(nc - row * p.Ns);
+    const int nh = p.nh, nl = nh + 1;
+    const float* film = p.film + row * nl * H;
+    float* ut = p.u + nc * nl * H;
+    const int q0 = wave * QW;
+    const int nblocks = nh * NB;
+
+    for (int f = threadIdx.x; f < H; f += 64 * KS) {
+        f4 w = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < p.d; ++k) w[k] = p.w0[f * p.d + k];
+        *(f4*)(w0s + 4 * f) = w;
+    }
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < p.d) {
+            float v = p.coords[(int64_t)sensor * p.d + k];
+            if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+            cn[k] = v;
+        }
+    }
+    __syncthreads();
+    if (nblocks > 0) siren_issue_block_u<NB, KS>(p.wimg16, 0, wbuf, wave, lane);
+
+    float X[QW][4], Xn[QW][4];
+    static_for<QW>([&](auto qc) {
+        constexpr int qq = decltype(qc)::value;
+        const int q = q0 + qq;
+        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
+        f4 uu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
+            float a = cn[0] * w[0];
+#pragma unroll
+            for (int k = 1; k < 4; ++k)
+                if (k < p.d) a = fmaf(cn[k], w[k], a);
+            uu[r] = a + fv[r];
+            X[qq][r] = sin_cw(p.w0f * uu[r]);
+        }
+        *(f4*)(ut + 16 * q + 4 * g) = uu;
+    });
+    Frag xh[QC], xl[QC];
+    auto split_x = [&]() __attribute__((always_inline)) {
+        static_for<QC>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            split8(X[2 * i], X[2 * i + 1], xh[i], xl[i]);
+        });
+    };
+    split_x();
+
+    int J = 0;
+    for (int layer = 1; layer <= nh; ++layer) {
+        const float inv = 1.0f / p.wscale[layer - 1];   // a power of two: exact
+        // this wave's FiLM rows of the layer (its own blocks), before the block loop: the
+        // loop's only vector-memory operations are then the DMA and the tape store
+        f4 fvr[QW];
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+            fvr[qq] = *(const f4*)(film + layer * H + 16 * (q0 + qq) + 4 * g);
+        });
+        static_for<NB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            constexpr int jp = j > 0 ? j - 1 : 0;   // the pending block (j > 0)
+            const bool own = j > 0 && jp / QW == wave;
+            if (J + 1 < nblocks) siren_issue_block_u<NB, KS>(p.wimg16, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            const float* wb = wbuf + (J & 1) * BLK;
+            h8 wh[QC], wl[QC];
+            static_for<QC>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int qg = q0 / 2 + i;
+                wh[i] = *(const h8*)(wb + qg * 512 + lane * 4);
+                wl[i] = *(const h8*)(wb + qg * 512 + 256 + lane * 4);
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            // the MFMA chain of block j, with the pending block's epilogue between its
+            // K-chunks (every wave computes it, the owner keeps it: no branch in the chain)
+            f4 a = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f};
+            float xs[4] = {0.f, 0.f, 0.f, 0.f};
+            static_for<QC>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[i], xh[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xl[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xh[i].h(), a, 0, 0, 0);
+                if constexpr (j > 0 && i == 0) {
+                    const float* rs = red + (jp & 1) * KS * 256;
+                    acc = *(const f4*)(rs + lane * 4);
+#pragma unroll
+                    for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+                    asm volatile("" : "+v"(acc));
+                }
+                if constexpr (j > 0 && i == (QC > 1 ? 1 : 0)) {
+                    acc = acc * inv + fvr[jp % QW];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xs[r] = sin_cw(p.w0f * acc[r]);
+                    // pinned here, between the MFMAs (else they sink into the owner's branch)
+                    asm volatile("" : "+v"(xs[0]), "+v"(xs[1]), "+v"(xs[2]), "+v"(xs[3]), "+v"(acc));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            if constexpr (j > 0) {
+                if (own) {
+                    *(f4*)(ut + layer * H + 16 * jp + 4 * g) = acc;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Xn[jp % QW][r] = xs[r];
+                }
+            }
+            *(f4*)(red + (j & 1) * KS * 256 + (wave * 64 + lane) * 4) = a;
+            // block J + 1 landed (this wave's pieces; the barrier covers the others') and
+            // the partial is in LDS; the owner's tape store may stay in flight.  A bare
+            // s_barrier: __syncthreads' fence would wait for that store.
+            if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(1));
+            else __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(0));
+            asm volatile("s_barrier" ::: "memory");
+            ++J;
+        });
+        // the layer's last block, after its barrier
+        if ((NB - 1) / QW == wave) {
+            constexpr int qq = (NB - 1) % QW;
+            const float* rs = red + ((NB - 1) & 1) * KS * 256;
+            f4 acc = *(const f4*)(rs + lane * 4);
+#pragma unroll
+            for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+            acc = acc * inv + fvr[qq];
+            *(f4*)(ut + layer * H + 16 * (NB - 1) + 4 * g) = acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Xn[qq][r] = sin_cw(p.w0f * acc[r]);
+        }
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[qq][r] = Xn[qq][r];
+        });
+        if (layer < nh) split_x();
+    }
+
+    // output layer in fp32: partial sums over this wave's features, combined in wave order
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            const float* wr = p.wout + oc * H + 4 * g;
+            float sm = 0.f;
+            static_for<QW>([&](auto qc) {
+                constexpr int qq = decltype(qc)::value;
+                const f4 w = *(const f4*)(wr + 16 * (q0 + qq));
+                sm = fmaf(w.x, X[qq][0], sm);
+                sm = fmaf(w.y, X[qq][1], sm);
+                sm = fmaf(w.z, X[qq][2], sm);
+                sm = fmaf(w.w, X[qq][3], sm);
+            });
+            sm += __shfl_xor(sm, 16);
+            sm += __shfl_xor(sm, 32);
+            if (g == 0) osum[(wave * 4 + oc) * 16 + j16] = sm;
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            float sm = osum[oc * 16 + j16];
+#pragma unroll
+            for (int w = 1; w < KS; ++w) sm += osum[(w * 4 + oc) * 16 + j16];
+            o[oc] = sm + p.bout[oc];
+        }
+    }
+    if (n < p.P && g < p.c) {
+        float v = g == 0 ? o[0] : g == 1 ? o[1] : g == 2 ? o[2] : o[3];
+        if (p.ymax) {
+            const int64_t yi = (int64_t)sensor * p.ystride + g;
+            const float hi = p.ymax[yi], lo = p.ymin[yi];
+            v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
+        }
+        p.out[n * p.c + g] = v;
+    }
+}
+
+template <int NB, int KS>
+__global__ __launch_bounds__(64 * KS) void siren_tape_bwd_split(SirenTapeArgs p) {
+    constexpr int H = NB * 16, BLK = NB * 256, QW = NB / KS, QC = QW / 2;
+    static_assert(QW % 2 == 0, "K9t: an even block count per wave");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* wbuf = smem;
+    float* red = smem + 2 * BLK;         // 2 x KS x 64 lanes x f4
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int sensor = (int)(nc % p.Ns);
+    const int nh = p.nh, nl = nh + 1;
+    const float* ut = p.u + nc * nl * H;
+    float* dt = p.delta + nc * nl * H;
+    const float w0f = p.w0f;
+    const int q0 = wave * QW;
+    const int nblocks = nh * NB;
+
+    if (nblocks > 0) siren_issue_block_u<NB, KS>(p.wimg16t, 0, wbuf, wave, lane);
+    float dy[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            float v = p.gout[nc * p.c + oc];
+            if (p.ymax) {
+                const int64_t yi = (int64_t)sensor * p.ystride + oc;
+                v = v * ((p.ymax[yi] - p.ymin[yi]) / 2.0f);
+            }
+            dy[oc] = v;
+        }
+    }
+    float X[QW][4], Xn[QW][4];
+    static_for<QW>([&](auto qc) {
+        constexpr int qq = decltype(qc)::value;
+        const int q = q0 + qq;
+        const f4 uu = *(const f4*)(ut + nh * H + 16 * q + 4 * g);
+        f4 dd;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = 16 * q + 4 * g + r;
+            float gx = 0.f;
+#pragma unroll
+            for (int oc = 0; oc < 4; ++oc)
+                if (oc < p.c) gx = fmaf(p.wout[oc * H + f], dy[oc], gx);
+            dd[r] = gx * (w0f * cos_cw(w0f * uu[r]));
+            X[qq][r] = dd[r];
+        }
+        *(f4*)(dt + nh * H + 16 * q + 4 * g) = dd;
+    });
+    // this wave's slice of a pair's deltas, scaled by 2^-e into [0.5, 1) and split;
+    // returns e (0 for an all-zero slice)
+    Frag xh[QC], xl[QC];
+    auto split_scaled = [&]() __attribute__((always_inline)) -> int {
+        float m = 0.f;
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(X[qq][r]));
+        });
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const int e = m > 0.f ? __builtin_amdgcn_frexp_expf(m) : 0;
+        static_for<QC>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            float x0[4], x1[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                x0[r] = __builtin_amdgcn_ldexpf(X[2 * i][r], -e);
+                x1[r] = __builtin_amdgcn_ldexpf(X[2 * i + 1][r], -e);
+            }
+            split8(x0, x1, xh[i], xl[i]);
+        });
+        return e;
+    };
+
+    int J = 0;
+    for (int layer = nh; layer >= 1; --layer) {
+        const int li = layer - 1;
+        const int e = split_scaled();
+        const float inv = 1.0f / p.wscale[li];   // a power of two: exact
+        f4 uur[QW];   // this wave's pre-activations of the layer (its own blocks)
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+            uur[qq] = *(const f4*)(ut + li * H + 16 * (q0 + qq) + 4 * g);
+        });
+        static_for<NB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            constexpr int jp = j > 0 ? j - 1 : 0;
+            const bool own = j > 0 && jp / QW == wave;
+            if (J + 1 < nblocks) siren_issue_block_u<NB, KS>(p.wimg16t, J + 1, wbuf + ((J + 1) & 1) * BLK, wave, lane);
+            const float* wb = wbuf + (J & 1) * BLK;
+            h8 wh[QC], wl[QC];
+            static_for<QC>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int qg = q0 / 2 + i;
+                wh[i] = *(const h8*)(wb + qg * 512 + lane * 4);
+                wl[i] = *(const h8*)(wb + qg * 512 + 256 + lane * 4);
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            f4 a = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f}, dd = {0.f, 0.f, 0.f, 0.f};
+            static_for<QC>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[i], xh[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xl[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xh[i].h(), a, 0, 0, 0);
+                if constexpr (j > 0 && i == 0) {
+                    const float* rs = red + (jp & 1) * KS * 256;
+                    acc = *(const f4*)(rs + lane * 4);
+#pragma unroll
+                    for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+                    asm volatile("" : "+v"(acc));
+                }
+                if constexpr (j > 0 && i == (QC > 1 ? 1 : 0)) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dd[r] = acc[r] * (w0f * cos_cw(w0f * uur[jp % QW][r]));
+                    asm volatile("" : "+v"(dd));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            if constexpr (j > 0) {
+                if (own) {
+                    *(f4*)(dt + li * H + 16 * jp + 4 * g) = dd;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Xn[jp % QW][r] = dd[r];
+                }
+            }
+            // back to the deltas' own scale: x 2^e / s (exact)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] = __builtin_amdgcn_ldexpf(a[r] * inv, e);
+            *(f4*)(red + (j & 1) * KS * 256 + (wave * 64 + lane) * 4) = a;
+            if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(1));
+            else __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(0));
+            asm volatile("s_barrier" ::: "memory");
+            ++J;
+        });
+        if ((NB - 1) / QW == wave) {
+            constexpr int qq = (NB - 1) % QW;
+            const float* rs = red + ((NB - 1) & 1) * KS * 256;
+            f4 acc = *(const f4*)(rs + lane * 4);
+#pragma unroll
+            for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+            f4 dd;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                dd[r] = acc[r] * (w0f * cos_cw(w0f * uur[qq][r]));
+                Xn[qq][r] = dd[r];
+            }
+            *(f4*)(dt + li * H + 16 * (NB - 1) + 4 * g) = dd;
+        }
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[qq][r] = Xn[qq][r];
+        });
+    }
+}
+
+namespace {
+template <int NB, int KS>
+void launch_tape_split_nb(const SirenTapeArgs& a, bool bwd, hipStream_t st) {
+    constexpr int H = NB * 16;
+    const size_t lds = sizeof(float) * ((size_t)2 * NB * 256 + 2 * KS * 256 + (bwd ? 0 : 4 * H + KS * 64));
+    const void* fn = bwd ? (const void*)siren_tape_bwd_split<NB, KS> : (const void*)siren_tape_fwd_split<NB, KS>;
+    CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const dim3 grid((unsigned)ceil_div(a.P, 16));
+    if (bwd)
+        hipLaunchKernelGGL((siren_tape_bwd_split<NB, KS>), grid, dim3(64 * KS), lds, st, a);
+    else
+        hipLaunchKernelGGL((siren_tape_fwd_split<NB, KS>), grid, dim3(64 * KS), lds, st, a);
+    check_launch(bwd ? "siren_tape_bwd_split" : "siren_tape_fwd_split");
+}
+}  // namespace
+
+// K9t takes 4 waves per tile where 4 divides the block count into even shares
+bool tape_split_supported(int NB) { return NB == 8 || NB == 16 || NB == 24; }
+
+void launch_tape_split(int NB, const SirenTapeArgs& a, bool bwd, hipStream_t st) {
+    CFD_REQUIRE(a.wimg16 && a.wimg16t && a.wscale, CFD_ESTATE, "internal: split tape images not set");
+    switch (NB) {
+        case 8: return launch_tape_split_nb<8, 4>(a, bwd, st);
+        case 16: return launch_tape_split_nb<16, 4>(a, bwd, st);
+        case 24: return launch_tape_split_nb<24, 4>(a, bwd, st);
+        default: throw Error{CFD_EARG, "split-f16 tape needs hidden_features in {128, 256, 384}"};
     }
 }
 

@@ -106,6 +106,59 @@ def test_siren_latent_vjp_matches_autograd(hip, dims, Ns, R):
     assert err < 1e-3, err
 
 
+def _tape_case(seed, dims, Ns, R):
+    d, L, c, nh, H = dims
+    sd_np = synth.siren_state_dict(seed, d, L, c, nh, H)
+    coords = torch.from_numpy(synth.uniform(seed, "c", (Ns, d), -0.5, 2.0))
+    xhi, xlo = torch.full((1, d), 2.2), torch.full((1, d), -0.7)
+    yhi = torch.from_numpy(synth.uniform(seed, "yhi", (c,), 0.5, 2.0))
+    z = torch.from_numpy(synth.normal(seed, "z", (R, L))) * 0.5
+    gout = torch.from_numpy(synth.normal(seed, "g", (R, Ns, c)))
+    return sd_np, coords, (xhi, xlo, yhi, -yhi), z, gout
+
+
+@pytest.mark.parametrize("dims", [(3, 64, 3, 15, 384), (2, 32, 2, 4, 128)], ids=["h384", "h128"])
+def test_split_tape_is_fp32_level_and_scale_exact(hip, dims):
+    """K9t (the split-f16 tape, the default at H = 128 / 256 / 384) against an fp64
+    autograd evaluation of the oracle: output and latent gradient within 2x the
+    exact-fp32 tape's own error (+1e-7 of the max); the backward's per-pair
+    power-of-two operand scaling makes the gradient exactly homogeneous under
+    power-of-two gradient scales (2^-40 .. 2^40, far outside f16's range); rows
+    taped alone equal the same rows taped in a larger batch, bit for bit (Ns = 10:
+    16-pair tiles straddle rows)."""
+    d, L, c, nh, H = dims
+    Ns, R = 10, 24
+    sd_np, coords, (xhi, xlo, yhi, ylo), z, gout = _tape_case(41, dims, Ns, R)
+    sd64 = {k: torch.from_numpy(v).double() for k, v in sd_np.items()}
+    z64 = z.double().requires_grad_()
+    ref = osn.decode(sd64, coords.double(), z64, xhi.double(), xlo.double(), yhi.double(), ylo.double())
+    (gz_ref,) = torch.autograd.grad(ref, z64, gout.double())
+    ref, gz_ref = ref.detach(), gz_ref.detach()
+    xn = Normalizer_ts(params=(xhi, xlo), method="-11", dim=0)
+    yn = Normalizer_ts(params=(yhi, ylo), method="-11", dim=0)
+    res = {}
+    for mode in ("f32", "split_f16"):
+        nf = SIRENAutodecoder_film(d, L, c, nh, H)
+        nf.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()})
+        nf.to(DEV).set_compute(mode)
+        out = nf.tape_forward(coords.to(DEV), z.to(DEV), xn, yn)
+        gz = nf.tape_vjp(gout.to(DEV))
+        res[mode] = (nf, out, gz)
+    eo = {m: float((res[m][1].cpu().double() - ref).abs().max()) for m in res}
+    eg = {m: float((res[m][2].cpu().double() - gz_ref).abs().max()) for m in res}
+    assert eo["split_f16"] <= 2 * eo["f32"] + 1e-7 * float(ref.abs().max()), eo
+    assert eg["split_f16"] <= 2 * eg["f32"] + 1e-7 * float(gz_ref.abs().max()), eg
+    nf, out, gz = res["split_f16"]
+    g = gout.to(DEV)
+    for k in (-40, -12, 12, 40):
+        nf.tape_forward(coords.to(DEV), z.to(DEV), xn, yn)
+        assert torch.equal(nf.tape_vjp(g * 2.0 ** k), gz * 2.0 ** k), k
+    # rows 5..8 alone: the same output and gradient bits
+    o2 = nf.tape_forward(coords.to(DEV), z[5:9].to(DEV), xn, yn)
+    g2 = nf.tape_vjp(g[5:9])
+    assert torch.equal(o2, out[5:9]) and torch.equal(g2, gz[5:9])
+
+
 # ---------------------------------------------------------------------------
 # the guided loop of the Case4 notebook vs the reference's recorded run
 # ---------------------------------------------------------------------------
