@@ -256,6 +256,8 @@ def setup_B(dev, rank, world, siren_compute, unet_compute, plan_batch=0):
     # tests/test_gpu_cfg.py::test_configB_full_256_step_trajectory[plan1])
     model.set_plan_batch(max(plan_batch, 0))
     nf.set_compute(siren_compute)
+    model.prepare(dev)   # weights packed and resident before any timed step
+    nf.prepare(dev)
     diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=STEPS)
     ax = torch.linspace(0, 1, GRID)
     coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3).to(dev)
@@ -482,6 +484,10 @@ def main_uncond(args, rank, world, dev):
     model.set_compute(c["unet"] if args.unet_compute == "split_f16" else args.unet_compute)
     model.set_plan_batch(c["plan_batch"] if args.plan_batch < 0 else args.plan_batch)
     nf.set_compute(args.siren_compute)
+    # weights packed and resident before any timed step (with --warmup 0 the first
+    # timed forward would otherwise pay the host-side packing)
+    model.prepare(dev)
+    nf.prepare(dev)
     diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=c["respacing"])
     nsteps = diff.num_timesteps
     if args.config == "E":
@@ -581,6 +587,7 @@ def setup_C(dev, rank, world, siren_compute):
     nf.to(dev)
     cdist.broadcast_module(nf)
     nf.set_compute(siren_compute)
+    nf.prepare(dev)
     coords, lat, ymax, ymin, (s, e) = c_inputs(rank, world, C_COORDS, C_LATENTS, c["L"])
     lat = lat.to(dev)
     if world > 1:   # latents travel from rank 0 (the sampler's output in a full pipeline)
@@ -660,6 +667,8 @@ def setup_dps(dev, rank, world, which, batch, plan_batch=-1):
     nf.to(dev)
     cdist.broadcast_module(m)
     cdist.broadcast_module(nf)
+    m.prepare(dev)
+    nf.prepare(dev)
     ns = 10
     coords = torch.from_numpy(synth.uniform(5, "dps/sensors", (ns, d), 0.0, 1.0))
     xn = Normalizer_ts(params=(torch.ones(1, d), torch.zeros(1, d)), method="-11", dim=0)

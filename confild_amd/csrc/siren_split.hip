@@ -829,85 +829,64 @@ void launch_siren_split(int NB, SirenArgs a, int b, hipStream_t st) {
 // Lanes past the last pair compute pair P - 1 again (same inputs, same bits), so
 // every tape store is issued by every lane and the vmcnt accounting is exact.
 // ---------------------------------------------------------------------------
-template <int NB, int KS, int RING = 2, int TP = 1>
+template <int NB, int KS, int RING>
 __global__ __launch_bounds__(64 * KS) void siren_tape_fwd_split(SirenTapeArgs p) {
     constexpr int H = NB * 16, BLK = NB * 256, QW = NB / KS, QC = QW / 2;
-    static_assert(QW % 2 == 0 && (RING == 2 || RING == 3) && (TP == 1 || TP == 2), "K9t shape");
+    static_assert(QW % 2 == 0 && (RING == 2 || RING == 3), "K9t: an even block count per wave");
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* wbuf = smem;                  // RING ring slots
-    float* w0s = smem + RING * BLK;      // (H, 4)
-    float* red = w0s + 4 * H;            // 2 x TP x KS x 64 lanes x f4 partial sums
-    float* osum = red + 2 * TP * KS * 256;   // TP x KS x 4 x 16
+    // RING ring slots, then 2 x KS x 64 lanes x f4 partial sums: 80 KiB at H = 384, RING = 3
+    // (two workgroups per CU)
+    float* wbuf = smem;
+    float* red = smem + RING * BLK;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int64_t row = nc / p.Ns;
+    const int sensor = (int)(nc - row * p.Ns);
     const int nh = p.nh, nl = nh + 1;
+    const float* film = p.film + row * nl * H;
+    float* ut = p.u + nc * nl * H;
     const int q0 = wave * QW;
     const int nblocks = nh * NB;
-    // TP tiles of 16 pairs per workgroup: each weight fragment read feeds TP MFMA chains
-    int64_t n[TP];
-    int sensor[TP];
-    const float* film[TP];
-    float* ut[TP];
-    float cn[TP][4];
-    static_for<TP>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        n[t] = ((int64_t)blockIdx.x * TP + t) * 16 + j16;
-        const int64_t nc = n[t] < p.P ? n[t] : p.P - 1;
-        const int64_t row = nc / p.Ns;
-        sensor[t] = (int)(nc - row * p.Ns);
-        film[t] = p.film + row * nl * H;
-        ut[t] = p.u + nc * nl * H;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float v = 0.f;
-            if (k < p.d) {
-                v = p.coords[(int64_t)sensor[t] * p.d + k];
-                if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
-            }
-            cn[t][k] = v;
-        }
-    });
 
-    for (int f = threadIdx.x; f < H; f += 64 * KS) {
-        f4 w = {0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < p.d; ++k) w[k] = p.w0[f * p.d + k];
-        *(f4*)(w0s + 4 * f) = w;
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < p.d) {
+            float v = p.coords[(int64_t)sensor * p.d + k];
+            if (p.xmax) v = (v - p.xmin[k]) / (p.xmax[k] - p.xmin[k]) * 2.0f - 1.0f;
+            cn[k] = v;
+        }
     }
-    __syncthreads();
 #pragma unroll
     for (int r = 0; r + 1 < RING; ++r)
         if (r < nblocks) siren_issue_block_u<NB, KS>(p.wimg16, r, wbuf + r * BLK, wave, lane);
 
-    float X[TP][QW][4], Xn[TP][QW][4];
-    static_for<TP>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        static_for<QW>([&](auto qc) {
-            constexpr int qq = decltype(qc)::value;
-            const int q = q0 + qq;
-            const f4 fv = *(const f4*)(film[t] + 16 * q + 4 * g);
-            f4 uu;
+    float X[QW][4], Xn[QW][4];
+    static_for<QW>([&](auto qc) {
+        constexpr int qq = decltype(qc)::value;
+        const int q = q0 + qq;
+        const f4 fv = *(const f4*)(film + 16 * q + 4 * g);
+        f4 uu;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const f4 w = *(const f4*)(w0s + 4 * (16 * q + 4 * g + r));
-                float a = cn[t][0] * w[0];
+        for (int r = 0; r < 4; ++r) {
+            const float* w = p.w0 + (16 * q + 4 * g + r) * p.d;   // layer 0 (d <= 4 inputs)
+            float a = cn[0] * w[0];
 #pragma unroll
-                for (int k = 1; k < 4; ++k)
-                    if (k < p.d) a = fmaf(cn[t][k], w[k], a);
-                uu[r] = a + fv[r];
-                X[t][qq][r] = sin_cw(p.w0f * uu[r]);
-            }
-            *(f4*)(ut[t] + 16 * q + 4 * g) = uu;
-        });
+            for (int k = 1; k < 4; ++k)
+                if (k < p.d) a = fmaf(cn[k], w[k], a);
+            uu[r] = a + fv[r];
+            X[qq][r] = sin_cw(p.w0f * uu[r]);
+        }
+        *(f4*)(ut + 16 * q + 4 * g) = uu;
     });
-    Frag xh[TP][QC], xl[TP][QC];
+    Frag xh[QC], xl[QC];
     auto split_x = [&]() __attribute__((always_inline)) {
-        static_for<TP>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            static_for<QC>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                split8(X[t][2 * i], X[t][2 * i + 1], xh[t][i], xl[t][i]);
-            });
+        static_for<QC>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            split8(X[2 * i], X[2 * i + 1], xh[i], xl[i]);
         });
     };
     split_x();
@@ -916,14 +895,11 @@ __global__ __launch_bounds__(64 * KS) void siren_tape_fwd_split(SirenTapeArgs p)
     for (int layer = 1; layer <= nh; ++layer) {
         const float inv = 1.0f / p.wscale[layer - 1];   // a power of two: exact
         // this wave's FiLM rows of the layer (its own blocks), before the block loop: the
-        // loop's only vector-memory operations are then the DMA and the tape stores
-        f4 fvr[TP][QW];
-        static_for<TP>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            static_for<QW>([&](auto qc) {
-                constexpr int qq = decltype(qc)::value;
-                fvr[t][qq] = *(const f4*)(film[t] + layer * H + 16 * (q0 + qq) + 4 * g);
-            });
+        // loop's only vector-memory operations are then the DMA and the tape store
+        f4 fvr[QW];
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+            fvr[qq] = *(const f4*)(film + layer * H + 16 * (q0 + qq) + 4 * g);
         });
         static_for<NB>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
@@ -941,71 +917,48 @@ __global__ __launch_bounds__(64 * KS) void siren_tape_fwd_split(SirenTapeArgs p)
                 wl[i] = *(const h8*)(wb + qg * 512 + 256 + lane * 4);
             });
             __builtin_amdgcn_sched_barrier(0);
-            // the MFMA chains of block j, with the pending block's epilogue between their
+            // the MFMA chain of block j, with the pending block's epilogue between its
             // K-chunks (every wave computes it, the owner keeps it: no branch in the chain)
-            f4 a[TP], acc[TP];
-            float xs[TP][4];
-            static_for<TP>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                a[t] = f4{0.f, 0.f, 0.f, 0.f};
-                acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) xs[t][r] = 0.f;
-            });
+            f4 a = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f};
+            float xs[4] = {0.f, 0.f, 0.f, 0.f};
             static_for<QC>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                static_for<TP>([&](auto tc) {
-                    constexpr int t = decltype(tc)::value;
-                    a[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[i], xh[t][i].h(), a[t], 0, 0, 0);
-                    a[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xl[t][i].h(), a[t], 0, 0, 0);
-                    a[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xh[t][i].h(), a[t], 0, 0, 0);
-                });
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[i], xh[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xl[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xh[i].h(), a, 0, 0, 0);
                 if constexpr (j > 0 && i == 0) {
-                    static_for<TP>([&](auto tc) {
-                        constexpr int t = decltype(tc)::value;
-                        const float* rs = red + ((jp & 1) * TP + t) * KS * 256;
-                        acc[t] = *(const f4*)(rs + lane * 4);
+                    const float* rs = red + (jp & 1) * KS * 256;
+                    acc = *(const f4*)(rs + lane * 4);
 #pragma unroll
-                        for (int w = 1; w < KS; ++w) acc[t] += *(const f4*)(rs + (w * 64 + lane) * 4);
-                        asm volatile("" : "+v"(acc[t]));
-                    });
+                    for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+                    asm volatile("" : "+v"(acc));
                 }
                 if constexpr (j > 0 && i == (QC > 1 ? 1 : 0)) {
-                    static_for<TP>([&](auto tc) {
-                        constexpr int t = decltype(tc)::value;
-                        acc[t] = acc[t] * inv + fvr[t][jp % QW];
+                    acc = acc * inv + fvr[jp % QW];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) xs[t][r] = sin_cw(p.w0f * acc[t][r]);
-                        // pinned here, between the MFMAs (else they sink into the owner's branch)
-                        asm volatile("" : "+v"(xs[t][0]), "+v"(xs[t][1]), "+v"(xs[t][2]), "+v"(xs[t][3]),
-                                     "+v"(acc[t]));
-                    });
+                    for (int r = 0; r < 4; ++r) xs[r] = sin_cw(p.w0f * acc[r]);
+                    // pinned here, between the MFMAs (else they sink into the owner's branch)
+                    asm volatile("" : "+v"(xs[0]), "+v"(xs[1]), "+v"(xs[2]), "+v"(xs[3]), "+v"(acc));
                 }
                 __builtin_amdgcn_sched_barrier(0);
             });
             if constexpr (j > 0) {
                 if (own) {
-                    static_for<TP>([&](auto tc) {
-                        constexpr int t = decltype(tc)::value;
-                        *(f4*)(ut[t] + layer * H + 16 * jp + 4 * g) = acc[t];
+                    *(f4*)(ut + layer * H + 16 * jp + 4 * g) = acc;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) Xn[t][jp % QW][r] = xs[t][r];
-                    });
+                    for (int r = 0; r < 4; ++r) Xn[jp % QW][r] = xs[r];
                 }
             }
-            static_for<TP>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                *(f4*)(red + ((j & 1) * TP + t) * KS * 256 + (wave * 64 + lane) * 4) = a[t];
-            });
+            *(f4*)(red + (j & 1) * KS * 256 + (wave * 64 + lane) * 4) = a;
             // block J + 1 landed (this wave's pieces; the barrier covers the others') and
-            // the partials are in LDS; in flight at most: the younger block's DMA (RING 3)
-            // and the owner's tape stores.  A bare s_barrier: __syncthreads' fence would
-            // wait for those stores.
+            // the partial is in LDS; the owner's tape store may stay in flight.  A bare
+            // s_barrier: __syncthreads' fence would wait for that store.
+            // in flight at most: the younger block's DMA (RING 3) and the tape store
             if (RING == 3 && ahead) {
-                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(QW + TP));
+                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(QW + 1));
                 else __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(QW));
             } else {
-                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(TP));
+                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(1));
                 else __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(0));
             }
             asm volatile("s_barrier" ::: "memory");
@@ -1014,180 +967,155 @@ __global__ __launch_bounds__(64 * KS) void siren_tape_fwd_split(SirenTapeArgs p)
         // the layer's last block, after its barrier
         if ((NB - 1) / QW == wave) {
             constexpr int qq = (NB - 1) % QW;
-            static_for<TP>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                const float* rs = red + (((NB - 1) & 1) * TP + t) * KS * 256;
-                f4 acc = *(const f4*)(rs + lane * 4);
+            const float* rs = red + ((NB - 1) & 1) * KS * 256;
+            f4 acc = *(const f4*)(rs + lane * 4);
 #pragma unroll
-                for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
-                acc = acc * inv + fvr[t][qq];
-                *(f4*)(ut[t] + layer * H + 16 * (NB - 1) + 4 * g) = acc;
+            for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+            acc = acc * inv + fvr[qq];
+            *(f4*)(ut + layer * H + 16 * (NB - 1) + 4 * g) = acc;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) Xn[t][qq][r] = sin_cw(p.w0f * acc[r]);
-            });
+            for (int r = 0; r < 4; ++r) Xn[qq][r] = sin_cw(p.w0f * acc[r]);
         }
-        static_for<TP>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            static_for<QW>([&](auto qc) {
-                constexpr int qq = decltype(qc)::value;
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) X[t][qq][r] = Xn[t][qq][r];
-            });
+            for (int r = 0; r < 4; ++r) X[qq][r] = Xn[qq][r];
         });
         if (layer < nh) split_x();
     }
 
     // output layer in fp32: partial sums over this wave's features, combined in wave order
-    static_for<TP>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
+    // (KS x 4 x 16 sums in the partial-sum slot the last block's epilogue does not read)
+    float* osum = red + (NB & 1) * KS * 256;
 #pragma unroll
-        for (int oc = 0; oc < 4; ++oc) {
-            if (oc < p.c) {
-                const float* wr = p.wout + oc * H + 4 * g;
-                float sm = 0.f;
-                static_for<QW>([&](auto qc) {
-                    constexpr int qq = decltype(qc)::value;
-                    const f4 w = *(const f4*)(wr + 16 * (q0 + qq));
-                    sm = fmaf(w.x, X[t][qq][0], sm);
-                    sm = fmaf(w.y, X[t][qq][1], sm);
-                    sm = fmaf(w.z, X[t][qq][2], sm);
-                    sm = fmaf(w.w, X[t][qq][3], sm);
-                });
-                sm += __shfl_xor(sm, 16);
-                sm += __shfl_xor(sm, 32);
-                if (g == 0) osum[((t * KS + wave) * 4 + oc) * 16 + j16] = sm;
-            }
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            const float* wr = p.wout + oc * H + 4 * g;
+            float sm = 0.f;
+            static_for<QW>([&](auto qc) {
+                constexpr int qq = decltype(qc)::value;
+                const f4 w = *(const f4*)(wr + 16 * (q0 + qq));
+                sm = fmaf(w.x, X[qq][0], sm);
+                sm = fmaf(w.y, X[qq][1], sm);
+                sm = fmaf(w.z, X[qq][2], sm);
+                sm = fmaf(w.w, X[qq][3], sm);
+            });
+            sm += __shfl_xor(sm, 16);
+            sm += __shfl_xor(sm, 32);
+            if (g == 0) osum[(wave * 4 + oc) * 16 + j16] = sm;
         }
-    });
+    }
     __syncthreads();
     if (wave != 0) return;
-    static_for<TP>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        float o[4] = {0.f, 0.f, 0.f, 0.f};
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int oc = 0; oc < 4; ++oc) {
-            if (oc < p.c) {
-                float sm = osum[((t * KS) * 4 + oc) * 16 + j16];
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            float sm = osum[oc * 16 + j16];
 #pragma unroll
-                for (int w = 1; w < KS; ++w) sm += osum[((t * KS + w) * 4 + oc) * 16 + j16];
-                o[oc] = sm + p.bout[oc];
-            }
+            for (int w = 1; w < KS; ++w) sm += osum[(w * 4 + oc) * 16 + j16];
+            o[oc] = sm + p.bout[oc];
         }
-        if (n[t] < p.P && g < p.c) {
-            float v = g == 0 ? o[0] : g == 1 ? o[1] : g == 2 ? o[2] : o[3];
-            if (p.ymax) {
-                const int64_t yi = (int64_t)sensor[t] * p.ystride + g;
-                const float hi = p.ymax[yi], lo = p.ymin[yi];
-                v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
-            }
-            p.out[n[t] * p.c + g] = v;
+    }
+    if (n < p.P && g < p.c) {
+        float v = g == 0 ? o[0] : g == 1 ? o[1] : g == 2 ? o[2] : o[3];
+        if (p.ymax) {
+            const int64_t yi = (int64_t)sensor * p.ystride + g;
+            const float hi = p.ymax[yi], lo = p.ymin[yi];
+            v = (v + 1.0f) / 2.0f * (hi - lo) + lo;
         }
-    });
+        p.out[n * p.c + g] = v;
+    }
 }
 
-template <int NB, int KS, int RING = 2, int TP = 1>
+template <int NB, int KS, int RING>
 __global__ __launch_bounds__(64 * KS) void siren_tape_bwd_split(SirenTapeArgs p) {
     constexpr int H = NB * 16, BLK = NB * 256, QW = NB / KS, QC = QW / 2;
-    static_assert(QW % 2 == 0 && (RING == 2 || RING == 3) && (TP == 1 || TP == 2), "K9t shape");
+    static_assert(QW % 2 == 0 && (RING == 2 || RING == 3), "K9t: an even block count per wave");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* wbuf = smem;
-    float* red = smem + RING * BLK;      // 2 x TP x KS x 64 lanes x f4
+    float* red = smem + RING * BLK;      // 2 x KS x 64 lanes x f4
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, j16 = lane & 15;
+    const int64_t n = (int64_t)blockIdx.x * 16 + j16;
+    const int64_t nc = n < p.P ? n : p.P - 1;
+    const int sensor = (int)(nc % p.Ns);
     const int nh = p.nh, nl = nh + 1;
+    const float* ut = p.u + nc * nl * H;
+    float* dt = p.delta + nc * nl * H;
     const float w0f = p.w0f;
     const int q0 = wave * QW;
     const int nblocks = nh * NB;
-    const float* ut[TP];
-    float* dt[TP];
-    float dy[TP][4];
-    static_for<TP>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        const int64_t n = ((int64_t)blockIdx.x * TP + t) * 16 + j16;
-        const int64_t nc = n < p.P ? n : p.P - 1;
-        const int sensor = (int)(nc % p.Ns);
-        ut[t] = p.u + nc * nl * H;
-        dt[t] = p.delta + nc * nl * H;
-#pragma unroll
-        for (int oc = 0; oc < 4; ++oc) {
-            float v = 0.f;
-            if (oc < p.c) {
-                v = p.gout[nc * p.c + oc];
-                if (p.ymax) {
-                    const int64_t yi = (int64_t)sensor * p.ystride + oc;
-                    v = v * ((p.ymax[yi] - p.ymin[yi]) / 2.0f);
-                }
-            }
-            dy[t][oc] = v;
-        }
-    });
 
 #pragma unroll
     for (int r = 0; r + 1 < RING; ++r)
         if (r < nblocks) siren_issue_block_u<NB, KS>(p.wimg16t, r, wbuf + r * BLK, wave, lane);
-    float X[TP][QW][4], Xn[TP][QW][4];
-    static_for<TP>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
+    float dy[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+        if (oc < p.c) {
+            float v = p.gout[nc * p.c + oc];
+            if (p.ymax) {
+                const int64_t yi = (int64_t)sensor * p.ystride + oc;
+                v = v * ((p.ymax[yi] - p.ymin[yi]) / 2.0f);
+            }
+            dy[oc] = v;
+        }
+    }
+    float X[QW][4], Xn[QW][4];
+    static_for<QW>([&](auto qc) {
+        constexpr int qq = decltype(qc)::value;
+        const int q = q0 + qq;
+        const f4 uu = *(const f4*)(ut + nh * H + 16 * q + 4 * g);
+        f4 dd;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = 16 * q + 4 * g + r;
+            float gx = 0.f;
+#pragma unroll
+            for (int oc = 0; oc < 4; ++oc)
+                if (oc < p.c) gx = fmaf(p.wout[oc * H + f], dy[oc], gx);
+            dd[r] = gx * (w0f * cos_cw(w0f * uu[r]));
+            X[qq][r] = dd[r];
+        }
+        *(f4*)(dt + nh * H + 16 * q + 4 * g) = dd;
+    });
+    // this wave's slice of a pair's deltas, scaled by 2^-e into [0.5, 1) and split;
+    // returns e (0 for an all-zero slice)
+    Frag xh[QC], xl[QC];
+    auto split_scaled = [&]() __attribute__((always_inline)) -> int {
+        float m = 0.f;
         static_for<QW>([&](auto qc) {
             constexpr int qq = decltype(qc)::value;
-            const int q = q0 + qq;
-            const f4 uu = *(const f4*)(ut[t] + nh * H + 16 * q + 4 * g);
-            f4 dd;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(X[qq][r]));
+        });
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const int e = m > 0.f ? __builtin_amdgcn_frexp_expf(m) : 0;
+        static_for<QC>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            float x0[4], x1[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int f = 16 * q + 4 * g + r;
-                float gx = 0.f;
-#pragma unroll
-                for (int oc = 0; oc < 4; ++oc)
-                    if (oc < p.c) gx = fmaf(p.wout[oc * H + f], dy[t][oc], gx);
-                dd[r] = gx * (w0f * cos_cw(w0f * uu[r]));
-                X[t][qq][r] = dd[r];
+                x0[r] = __builtin_amdgcn_ldexpf(X[2 * i][r], -e);
+                x1[r] = __builtin_amdgcn_ldexpf(X[2 * i + 1][r], -e);
             }
-            *(f4*)(dt[t] + nh * H + 16 * q + 4 * g) = dd;
+            split8(x0, x1, xh[i], xl[i]);
         });
-    });
-    // this wave's slice of a pair's deltas, scaled by 2^-e into [0.5, 1) and split
-    // (per tile: e is per pair and wave; 0 for an all-zero slice)
-    Frag xh[TP][QC], xl[TP][QC];
-    int e[TP];
-    auto split_scaled = [&]() __attribute__((always_inline)) {
-        static_for<TP>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            float m = 0.f;
-            static_for<QW>([&](auto qc) {
-                constexpr int qq = decltype(qc)::value;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(X[t][qq][r]));
-            });
-            m = fmaxf(m, __shfl_xor(m, 16));
-            m = fmaxf(m, __shfl_xor(m, 32));
-            e[t] = m > 0.f ? __builtin_amdgcn_frexp_expf(m) : 0;
-            static_for<QC>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                float x0[4], x1[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    x0[r] = __builtin_amdgcn_ldexpf(X[t][2 * i][r], -e[t]);
-                    x1[r] = __builtin_amdgcn_ldexpf(X[t][2 * i + 1][r], -e[t]);
-                }
-                split8(x0, x1, xh[t][i], xl[t][i]);
-            });
-        });
+        return e;
     };
 
     int J = 0;
     for (int layer = nh; layer >= 1; --layer) {
         const int li = layer - 1;
-        split_scaled();
+        const int e = split_scaled();
         const float inv = 1.0f / p.wscale[li];   // a power of two: exact
-        f4 uur[TP][QW];   // this wave's pre-activations of the layer (its own blocks)
-        static_for<TP>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            static_for<QW>([&](auto qc) {
-                constexpr int qq = decltype(qc)::value;
-                uur[t][qq] = *(const f4*)(ut[t] + li * H + 16 * (q0 + qq) + 4 * g);
-            });
+        f4 uur[QW];   // this wave's pre-activations of the layer (its own blocks)
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
+            uur[qq] = *(const f4*)(ut + li * H + 16 * (q0 + qq) + 4 * g);
         });
         static_for<NB>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
@@ -1205,65 +1133,43 @@ __global__ __launch_bounds__(64 * KS) void siren_tape_bwd_split(SirenTapeArgs p)
                 wl[i] = *(const h8*)(wb + qg * 512 + 256 + lane * 4);
             });
             __builtin_amdgcn_sched_barrier(0);
-            f4 a[TP], acc[TP], dd[TP];
-            static_for<TP>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                a[t] = f4{0.f, 0.f, 0.f, 0.f};
-                acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-                dd[t] = f4{0.f, 0.f, 0.f, 0.f};
-            });
+            f4 a = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f}, dd = {0.f, 0.f, 0.f, 0.f};
             static_for<QC>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                static_for<TP>([&](auto tc) {
-                    constexpr int t = decltype(tc)::value;
-                    a[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[i], xh[t][i].h(), a[t], 0, 0, 0);
-                    a[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xl[t][i].h(), a[t], 0, 0, 0);
-                    a[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xh[t][i].h(), a[t], 0, 0, 0);
-                });
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[i], xh[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xl[i].h(), a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i], xh[i].h(), a, 0, 0, 0);
                 if constexpr (j > 0 && i == 0) {
-                    static_for<TP>([&](auto tc) {
-                        constexpr int t = decltype(tc)::value;
-                        const float* rs = red + ((jp & 1) * TP + t) * KS * 256;
-                        acc[t] = *(const f4*)(rs + lane * 4);
+                    const float* rs = red + (jp & 1) * KS * 256;
+                    acc = *(const f4*)(rs + lane * 4);
 #pragma unroll
-                        for (int w = 1; w < KS; ++w) acc[t] += *(const f4*)(rs + (w * 64 + lane) * 4);
-                        asm volatile("" : "+v"(acc[t]));
-                    });
+                    for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+                    asm volatile("" : "+v"(acc));
                 }
                 if constexpr (j > 0 && i == (QC > 1 ? 1 : 0)) {
-                    static_for<TP>([&](auto tc) {
-                        constexpr int t = decltype(tc)::value;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            dd[t][r] = acc[t][r] * (w0f * cos_cw(w0f * uur[t][jp % QW][r]));
-                        asm volatile("" : "+v"(dd[t]));
-                    });
+                    for (int r = 0; r < 4; ++r) dd[r] = acc[r] * (w0f * cos_cw(w0f * uur[jp % QW][r]));
+                    asm volatile("" : "+v"(dd));
                 }
                 __builtin_amdgcn_sched_barrier(0);
             });
             if constexpr (j > 0) {
                 if (own) {
-                    static_for<TP>([&](auto tc) {
-                        constexpr int t = decltype(tc)::value;
-                        *(f4*)(dt[t] + li * H + 16 * jp + 4 * g) = dd[t];
+                    *(f4*)(dt + li * H + 16 * jp + 4 * g) = dd;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) Xn[t][jp % QW][r] = dd[t][r];
-                    });
+                    for (int r = 0; r < 4; ++r) Xn[jp % QW][r] = dd[r];
                 }
             }
             // back to the deltas' own scale: x 2^e / s (exact)
-            static_for<TP>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) a[t][r] = __builtin_amdgcn_ldexpf(a[t][r] * inv, e[t]);
-                *(f4*)(red + ((j & 1) * TP + t) * KS * 256 + (wave * 64 + lane) * 4) = a[t];
-            });
-            // in flight at most: the younger block's DMA (RING 3) and the tape stores
+            for (int r = 0; r < 4; ++r) a[r] = __builtin_amdgcn_ldexpf(a[r] * inv, e);
+            *(f4*)(red + (j & 1) * KS * 256 + (wave * 64 + lane) * 4) = a;
+            // in flight at most: the younger block's DMA (RING 3) and the tape store
             if (RING == 3 && ahead) {
-                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(QW + TP));
+                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(QW + 1));
                 else __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(QW));
             } else {
-                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(TP));
+                if (own) __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(1));
                 else __builtin_amdgcn_s_waitcnt(vm_lgkm0_imm(0));
             }
             asm volatile("s_barrier" ::: "memory");
@@ -1271,52 +1177,43 @@ __global__ __launch_bounds__(64 * KS) void siren_tape_bwd_split(SirenTapeArgs p)
         });
         if ((NB - 1) / QW == wave) {
             constexpr int qq = (NB - 1) % QW;
-            static_for<TP>([&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                const float* rs = red + (((NB - 1) & 1) * TP + t) * KS * 256;
-                f4 acc = *(const f4*)(rs + lane * 4);
+            const float* rs = red + ((NB - 1) & 1) * KS * 256;
+            f4 acc = *(const f4*)(rs + lane * 4);
 #pragma unroll
-                for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
-                f4 dd;
+            for (int w = 1; w < KS; ++w) acc += *(const f4*)(rs + (w * 64 + lane) * 4);
+            f4 dd;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    dd[r] = acc[r] * (w0f * cos_cw(w0f * uur[t][qq][r]));
-                    Xn[t][qq][r] = dd[r];
-                }
-                *(f4*)(dt[t] + li * H + 16 * (NB - 1) + 4 * g) = dd;
-            });
+            for (int r = 0; r < 4; ++r) {
+                dd[r] = acc[r] * (w0f * cos_cw(w0f * uur[qq][r]));
+                Xn[qq][r] = dd[r];
+            }
+            *(f4*)(dt + li * H + 16 * (NB - 1) + 4 * g) = dd;
         }
-        static_for<TP>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            static_for<QW>([&](auto qc) {
-                constexpr int qq = decltype(qc)::value;
+        static_for<QW>([&](auto qc) {
+            constexpr int qq = decltype(qc)::value;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) X[t][qq][r] = Xn[t][qq][r];
-            });
+            for (int r = 0; r < 4; ++r) X[qq][r] = Xn[qq][r];
         });
     }
 }
 
 namespace {
-#ifndef CFD_K9T_RING
-#define CFD_K9T_RING 2
-#endif
-#ifndef CFD_K9T_TP
-#define CFD_K9T_TP 1
-#endif
+// RING 3: two blocks' DMA ahead of the MFMAs (80 KiB of LDS at H = 384: still two
+// workgroups per CU).  Measured per DPS step (tools/dev/tape_bench.py, one box):
+// against RING 2 the VJP 0.41 -> 0.35 ms (config D) and 0.31 -> 0.25 ms (Case4);
+// two 16-pair tiles per workgroup (every weight fragment read feeding two MFMA
+// chains) measured no faster at D and 25 % slower at Case4 (half the workgroups).
 template <int NB, int KS>
 void launch_tape_split_nb(const SirenTapeArgs& a, bool bwd, hipStream_t st) {
-    constexpr int H = NB * 16, RING = CFD_K9T_RING, TP = CFD_K9T_TP;
-    const size_t lds =
-        sizeof(float) * ((size_t)RING * NB * 256 + 2 * TP * KS * 256 + (bwd ? 0 : 4 * H + TP * KS * 64));
-    const void* fn = bwd ? (const void*)siren_tape_bwd_split<NB, KS, RING, TP>
-                         : (const void*)siren_tape_fwd_split<NB, KS, RING, TP>;
+    constexpr int RING = 3;
+    const size_t lds = sizeof(float) * ((size_t)RING * NB * 256 + 2 * KS * 256);
+    const void* fn = bwd ? (const void*)siren_tape_bwd_split<NB, KS, RING> : (const void*)siren_tape_fwd_split<NB, KS, RING>;
     CFD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const dim3 grid((unsigned)ceil_div(a.P, 16 * TP));
+    const dim3 grid((unsigned)ceil_div(a.P, 16));
     if (bwd)
-        hipLaunchKernelGGL((siren_tape_bwd_split<NB, KS, RING, TP>), grid, dim3(64 * KS), lds, st, a);
+        hipLaunchKernelGGL((siren_tape_bwd_split<NB, KS, RING>), grid, dim3(64 * KS), lds, st, a);
     else
-        hipLaunchKernelGGL((siren_tape_fwd_split<NB, KS, RING, TP>), grid, dim3(64 * KS), lds, st, a);
+        hipLaunchKernelGGL((siren_tape_fwd_split<NB, KS, RING>), grid, dim3(64 * KS), lds, st, a);
     check_launch(bwd ? "siren_tape_bwd_split" : "siren_tape_fwd_split");
 }
 }  // namespace

@@ -105,6 +105,15 @@ class SIRENAutodecoder_film(nn.Module):
         return {v_: k for k, v_ in self.COMPUTE_MODES.items()}[v.value]
 
     # -- device handle --------------------------------------------------------
+    def prepare(self, device=None):
+        """Upload and pack the parameters into the device handle now (the first
+        decode does it otherwise).  Returns self."""
+        dev = torch.device(device) if device is not None else next(self.parameters()).device
+        if dev.type != "cuda":
+            raise _lib.CfdError("SIRENAutodecoder_film.prepare needs a GPU device")
+        self._handle(dev)
+        return self
+
     def _signature(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters())
 

@@ -303,6 +303,16 @@ class UNetModel(nn.Module):
         self.plan_batch = int(nominal_batch)
         return self
 
+    def prepare(self, device=None):
+        """Upload and pack the parameters into the device handle now (the first
+        forward does it otherwise): a timed region can then start with the weights
+        resident in HBM.  Returns self."""
+        dev = torch.device(device) if device is not None else next(self.parameters()).device
+        if dev.type != "cuda":
+            raise _lib.CfdError("UNetModel.prepare needs a GPU device")
+        self._handle(dev)
+        return self
+
     def _signature(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
