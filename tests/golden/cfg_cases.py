@@ -29,6 +29,10 @@ TRAJ_E = dict(tag="trajE", seed=1234, image_size=128, segments=((999, 20), (19, 
 # (indices 599..500), so the bf16 operands' drift is stated over 100 steps
 TRAJ_E100 = dict(tag="trajE100", start=599, n=100, keep=tuple(range(0, 100, 10)) + (99,))
 
+# config E, the whole loop (round 6): all 1000 steps (999..0) of the same loop from
+# a seeded x_T, so the bf16 operands' drift is stated over the line's full sampling
+TRAJ_E1000 = dict(tag="trajE1000", keep=tuple(range(0, 1000, 100)) + (999,))
+
 # config A (configs[0]): Case1 uncond 32^2 mult (1,2,3,4), DDIM-50, 1k-coord decode
 CFG_A = dict(tag="cfgA", seed=1234, image_size=32, respacing="ddim50", vmax=1.5, vmin=-1.5,
              unet=dict(image_size=32, num_channels=128, num_res_blocks=2, channel_mult="1,2,3,4", num_heads=4,

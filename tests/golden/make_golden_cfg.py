@@ -67,7 +67,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from confild_amd import synth  # noqa: E402
-from cfg_cases import (CASE4_OP, CASE4_STEPS, CFG_A, CNF_INF, DPS_D, POST, TRAJ_B, TRAJ_E, TRAJ_E100,  # noqa: E402
+from cfg_cases import (CASE4_OP, CASE4_STEPS, CFG_A, CNF_INF, DPS_D, POST, TRAJ_B, TRAJ_E, TRAJ_E100, TRAJ_E1000,  # noqa: E402
                        case4_files,
                        cnf_inference_coords, cnf_inference_files, noise_for, post_inputs, unet_weights)
 
@@ -181,6 +181,32 @@ def gen_trajE100():
     keep = list(c["keep"])
     _save("golden_trajE100.npz", keep=np.array(keep, dtype=np.int64), samples=np.stack([samples[k] for k in keep]),
           pred_xstart=np.stack([x0s[k] for k in keep]))
+
+
+def gen_trajE1000():
+    """config E: the whole 1000-step DDPM loop (999..0) of the 128^2 U-Net through
+    the reference's p_sample, B = 1, from a seeded x_T; sample and x0_hat every
+    100 steps and at the end."""
+    from src.script_util import create_gaussian_diffusion
+    c = TRAJ_E1000
+    m = _ref_unet(TRAJ_E["unet"], TRAJ_E["seed"])
+    diff = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing="")
+    S = TRAJ_E["image_size"]
+    shape = (1, 1, S, S)
+    x = torch.from_numpy(noise_for(f"{c['tag']}/x", 0, shape))
+    keep = list(c["keep"])
+    samples, x0s = [], []
+    t0 = time.time()
+    with _Noise(f"{c['tag']}/steps"), torch.no_grad():
+        for k, i in enumerate(range(999, -1, -1)):
+            out = diff.p_sample(m, x, torch.tensor([i]), clip_denoised=True)
+            x = out["sample"]
+            if k in keep:
+                samples.append(x.numpy())
+                x0s.append(out["pred_xstart"].numpy())
+    print(f"trajE1000: 1000 steps in {time.time() - t0:.1f} s")
+    _save("golden_trajE1000.npz", keep=np.array(keep, dtype=np.int64), samples=np.stack(samples),
+          pred_xstart=np.stack(x0s))
 
 
 # ---------------------------------------------------------------------------
@@ -423,7 +449,7 @@ def gen_post():
     _save("golden_post.npz", frames=frames.astype(np.float32), nan_frame=nanf.astype(np.float32))
 
 
-GEN = {"trajB": gen_trajB, "trajE": gen_trajE, "trajE100": gen_trajE100, "case4steps": gen_case4steps, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps,
+GEN = {"trajB": gen_trajB, "trajE": gen_trajE, "trajE100": gen_trajE100, "trajE1000": gen_trajE1000, "case4steps": gen_case4steps, "cfgA": gen_cfgA, "dpsD": gen_dpsD, "case4op": gen_case4op, "case4dps": gen_case4dps,
        "cnfinf": gen_cnfinf, "post": gen_post}
 
 if __name__ == "__main__":

@@ -59,7 +59,7 @@ def bench_siren(latents=64, npts=64 ** 3, dims=(3, 64, 3, 15, 384), iters=3, com
                       "tflops": flops / (best / 1e3) / 1e12}), flush=True)
 
 
-def bench_unet(batch=8, size=64, iters=10, bf16=False, compute=None, mult=""):
+def bench_unet(batch=8, size=64, iters=10, bf16=False, compute=None, mult="", plan=0):
     from confild_amd.script_util import create_model
     m = create_model(image_size=size, num_channels=128, num_res_blocks=2, num_heads=4, num_head_channels=64,
                      attention_resolutions="32,16,8", use_bf16=bf16, channel_mult=mult)
@@ -68,11 +68,12 @@ def bench_unet(batch=8, size=64, iters=10, bf16=False, compute=None, mult=""):
     m.to(DEV)
     if compute:
         m.set_compute(compute)
+    m.set_plan_batch(plan)
     x = torch.randn(batch, 1, size, size, device=DEV)
     t = torch.full((batch,), 500, dtype=torch.int64, device=DEV)
     med, best = timeit(lambda: m(x, t), iters=iters, warm=2)
     gf = {32: 19.23, 64: 68.61, 128: 140.75}.get(size, float("nan"))
-    print(json.dumps({"kernel": "unet_forward", "compute": m.compute, "batch": batch, "size": size, "ms": med,
+    print(json.dumps({"kernel": "unet_forward", "compute": m.compute, "batch": batch, "size": size, "plan": plan, "ms": med,
                       "best_ms": best,
                       "tflops": batch * gf * 1e9 / (best / 1e3) / 1e12}), flush=True)
 
@@ -194,11 +195,12 @@ if __name__ == "__main__":
     ap.add_argument("--compute", choices=["f32", "split_f16"], default=None)
     ap.add_argument("--unet-compute", choices=["fp32", "split_f16", "bf16"], default=None)
     ap.add_argument("--dims", default="3,64,3,15,384", help="SIREN d,L,c,nh,H")
+    ap.add_argument("--plan", type=int, default=0, help="U-Net planned batch (0: 8)")
     a = ap.parse_args()
     if a.what in ("siren", "sweep"):
         bench_siren(a.latents, dims=tuple(int(v) for v in a.dims.split(",")), compute=a.compute)
     if a.what in ("unet", "sweep"):
-        bench_unet(a.batch, a.size, bf16=a.bf16, compute=a.unet_compute, mult=a.mult)
+        bench_unet(a.batch, a.size, bf16=a.bf16, compute=a.unet_compute, mult=a.mult, plan=a.plan)
     if a.what == "dps":
         bench_dps(a.batch, a.size)
     if a.what == "train":
