@@ -453,7 +453,7 @@ def step_B(o, dev, seed, start, count, ev=None):
 UNCOND_CFG = {
     "A": dict(size=32, channel_mult="1,2,3,4", respacing="ddim50", ddim=True, batch=1,
               siren=dict(d=2, L=32, c=3, nh=10, H=128), coords=1000, unet="split_f16",
-              gflops=19.23, plan_batch=0),
+              gflops=19.23, plan_batch=1),   # one sample per GPU: planned for 1 (pinned by test_gpu_cfg.py)
     "E": dict(size=128, channel_mult="", respacing="", ddim=False, batch=8,
               siren=dict(d=2, L=128, c=2, nh=17, H=256), coords=256 * 256, unet="bf16",
               gflops=140.75, plan_batch=0),
@@ -552,7 +552,8 @@ def main_uncond(args, rank, world, dev):
                                        f"{c['channel_mult'] or 'default'}), {'DDIM-50' if c['ddim'] else 'DDPM'} "
                                        f"{nsteps} steps, {batch}/GPU, CNF SIREN({sc['d']},{sc['L']},{sc['c']},"
                                        f"{sc['nh']},{sc['H']}) decode of {Sz} latent rows per sample on {N} coords"),
-                          "global_batch": glob, "seq_len": Sz, "parallelism": f"dp{world} ({batch} samples per GPU)"},
+                          "global_batch": glob, "seq_len": Sz, "parallelism": f"dp{world} ({batch} samples per GPU)",
+                          "plan_batch": model.plan_batch or 8},
                "roofline": {"bound": "mfma", "kernel": f"{kname} (+siren_film)",
                             "achieved": flops / (dec_ms / 1e3) / 1e12, "peak": peak, "peak_basis": peak_basis,
                             "unit": "TFLOP/s", "frac": flops / (dec_ms / 1e3) / 1e12 / peak, "traffic": None,

@@ -349,8 +349,11 @@ struct Sizes {
     size_t max_act = 0, max_qkv = 0, max_cat = 0, max_att = 0;  // floats per sample
     size_t max_kvf = 0;  // split attention's packed K/V fragments (any level)
     size_t max_abw = 0;  // split attention backward's packs and scales (attention levels)
+    size_t max_apart = 0;  // key-chunked attention's partials (attention_kv_chunks > 1)
     std::vector<size_t> hs;                                     // skip-stack tensors, floats per sample
 };
+
+int plan_batch(const cfd_unet* h);
 
 Sizes sizes(const cfd_unet* h) {
     const auto& c = h->cfg;
@@ -368,8 +371,11 @@ Sizes sizes(const cfd_unet* h) {
         z.max_cat = std::max(z.max_cat, (size_t)hw * hw * (co + cmax));
         z.max_att = std::max(z.max_att, (size_t)hw * hw * co);  // heads * T <= C * T
         z.max_kvf = std::max(z.max_kvf, cfd::attention_split_floats(hw * hw, co));
-        if (has_attn(h, 1 << l) || l == c.n_mult - 1)   // (the middle block attends at the last level)
+        if (has_attn(h, 1 << l) || l == c.n_mult - 1) {   // (the middle block attends at the last level)
             z.max_abw = std::max(z.max_abw, cfd::attention_bwd_split_floats(hw * hw, co));
+            const int heads = c.num_head_channels == -1 ? c.num_heads : co / c.num_head_channels;
+            z.max_apart = std::max(z.max_apart, cfd::attention_part_floats(hw * hw, co, co / heads, plan_batch(h)));
+        }
         for (int r = 0; r < c.num_res_blocks; ++r) z.hs.push_back((size_t)hw * hw * co);
         ch = co;
         if (l != c.n_mult - 1) {
@@ -427,6 +433,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
     float* nbuf = ws.take((size_t)B * z.max_cat);
     float* splitk = ws.take(kSplitCap);
     float* kvws = ws.take((size_t)B * z.max_kvf);
+    float* apart = z.max_apart ? ws.take((size_t)B * z.max_apart) : nullptr;
     float* pool[3];
     for (auto& p : pool) p = ws.take((size_t)B * z.max_act);
     float* tmp = ws.take((size_t)B * z.max_act);
@@ -708,6 +715,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                          kv_packed = true;
                      });
                 cfd::AttnArgs aa{qb, ob, T, at.C, attn_scale, nullptr};
+                aa.part = apart;
                 if (tape) aa.lse = keep((size_t)B * at.heads * T);
                 rec.qkv = qb;
                 rec.o = ob;
@@ -719,7 +727,7 @@ void run(const cfd_unet* h, const float* x, const int64_t* t, float* eps, int B,
                     // softmax (unet.py:349-353), so fp32-level attention is within it; the exact
                     // fp32-MFMA kernel K4 stays for CFD_COMPUTE_F32
                     if (split_attn)
-                        cfd::launch_attention_split(aa, at.ch, at.heads, B, kvws, st, kv_packed);
+                        cfd::launch_attention_split(aa, at.ch, at.heads, B, plan_batch(h), kvws, st, kv_packed);
                     else
                         cfd::launch_attention(aa, at.ch, at.heads, B, st);
                 }

@@ -1516,7 +1516,7 @@ __global__ __launch_bounds__(256) void attn_kv_split_kernel(AttnArgs a, int CH, 
 // whole K/V of its (sample, head) from L2 (1 GB of L2 reads per 32^2 attention at
 // config B, its bound); K4d computes the same fragments in the same MFMA order
 // with the same softmax, bit-identical to it.
-template <int CH, int WAVES, int NS = 3>
+template <int CH, int WAVES, int NS = 3, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, const h8v* __restrict__ kf,
                                                                    const h8v* __restrict__ vf) {
     constexpr int NJ = CH / 32, ND = CH / 16;
@@ -1533,7 +1533,11 @@ __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, c
     int qt = blockIdx.x, h = blockIdx.y;
     int64_t b = blockIdx.z;
     const int heads = gridDim.y;
-    if (a.xcdmap) {
+    // SPLIT: grid.z = B x kc, this workgroup's key chunk kc_i of its (sample, head)
+    const int kcs = SPLIT ? a.kc : 1;
+    const int kc_i = SPLIT ? (int)(blockIdx.z % kcs) : 0;
+    if (SPLIT) b = blockIdx.z / kcs;
+    if (!SPLIT && a.xcdmap) {
         const int nt = gridDim.x;
         const int L = blockIdx.x + nt * (blockIdx.y + heads * blockIdx.z);
         const int r = L >> 3, grp = (r / nt) * 8 + (L & 7);
@@ -1561,10 +1565,12 @@ __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, c
                                              (__attribute__((address_space(3))) void*)&ring[stage][piece * 64], 16, 0, 0);
         }
     };
-    const int nblk = T32 / 32;
+    // key blocks [blk0, blk0 + nblk) of this workgroup (all of them unless SPLIT)
+    const int nall = T32 / 32, per = (nall + kcs - 1) / kcs;
+    const int blk0 = kc_i * per, nblk = min(per, nall - blk0);
 #pragma unroll
     for (int i = 0; i < NS - 1; ++i)
-        if (i < nblk) issue(32 * i, i);
+        if (i < nblk) issue(32 * (blk0 + i), i);
 
     h8v qh[NJ], ql[NJ];
     {
@@ -1584,7 +1590,7 @@ __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, c
     float mrun = -INFINITY, lrun = 0.f;
 
     for (int ib = 0; ib < nblk; ++ib) {
-        const int kb = 32 * ib, stage = ib % NS;
+        const int kb = 32 * (blk0 + ib), stage = ib % NS;
         // this wave's pieces of block ib landed (the blocks issued after it may
         // still fly), then the barrier publishes every wave's pieces and retires
         // every read of the stage refilled below (block ib - 1's)
@@ -1651,6 +1657,19 @@ __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, c
     }
     if (!active) return;
     const int tq = q0 + li;
+    if constexpr (SPLIT) {   // this chunk's unnormalised O and its (max, sum), for attn_combine_kernel
+        if (tq < T) {
+            const int64_t row = ((int64_t)kc_i * (gridDim.z / kcs) + b) * heads + h;
+            float* op = a.part + (row * T + tq) * CH;
+#pragma unroll
+            for (int d = 0; d < ND; ++d) *(f4*)(op + 16 * d + 4 * g) = O[d];
+            if (g == 0) {
+                float* ml = a.part + (int64_t)kcs * (gridDim.z / kcs) * heads * T * CH;
+                *(float2*)(ml + 2 * (row * T + tq)) = float2{mrun, lrun};
+            }
+        }
+        return;
+    }
     if (a.lse && g == 0 && tq < T)
         a.lse[((int64_t)b * gridDim.y + h) * T + tq] = (mrun + log2f(lrun)) * 0.69314718055994530942f;
     if (tq < T) {
@@ -1662,6 +1681,38 @@ __global__ __launch_bounds__(64 * WAVES) void attention_dma_kernel(AttnArgs a, c
             *(f4*)(op + 16 * d + 4 * g) = v;
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// The key-chunked attention's combine pass: per (sample, head, query) the kc
+// chunks' (max m_c, sum l_c, unnormalised O_c) in chunk order, M = max m_c,
+// O = sum 2^(m_c - M) O_c / sum 2^(m_c - M) l_c (base 2, as the kernel's softmax);
+// the log-sum-exp for the backward where it is kept.  One thread per 4 channels.
+template <int CH>
+__global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a, int heads, int B) {
+    constexpr int Q = CH / 4;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t rows = (int64_t)B * heads * a.T;
+    if (i >= rows * Q) return;
+    const int d4 = (int)(i % Q);
+    const int64_t r = i / Q;   // (b, h, q) row
+    const int kc = a.kc;
+    const float* ml = a.part + (int64_t)kc * rows * CH;
+    float M = -INFINITY;
+    for (int c = 0; c < kc; ++c) M = fmaxf(M, ml[2 * (c * rows + r)]);
+    float L = 0.f;
+    f4 o = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < kc; ++c) {
+        const float w = __builtin_amdgcn_exp2f(ml[2 * (c * rows + r)] - M);
+        L += w * ml[2 * (c * rows + r) + 1];
+        o += w * *(const f4*)(a.part + (c * rows + r) * CH + 4 * d4);
+    }
+    const int tq = (int)(r % a.T);
+    const int64_t bh = r / a.T;
+    const int h = (int)(bh % heads);
+    const int64_t b = bh / heads;
+    *(f4*)(a.out + (b * (int64_t)a.T + tq) * a.C + (int64_t)h * CH + 4 * d4) = o * (1.0f / L);
+    if (a.lse && d4 == 0) a.lse[bh * a.T + tq] = (M + log2f(L)) * 0.69314718055994530942f;
 }
 
 // ---------------------------------------------------------------------------
@@ -2129,7 +2180,33 @@ int64_t attention_split_voff(int T, int CH, int heads, int B) {
     return (int64_t)B * heads * (T32 / 16) * (CH / 32) * 128;
 }
 
-void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st, bool packed) {
+// Key chunks: where the planned batch's 4-wave grid has at most 128 workgroups
+// (planned batch 1-2 at 32^2 and below), the keys of each (sample, head) are split
+// into kc chunks of >= 2 blocks (kc x the grid <= 256), each a workgroup of its own,
+// and a combine pass adds the chunks' softmax partials in chunk order.  A function
+// of T, heads and the planned batch only (never of the real batch): a sample's bits
+// stay batch-invariant for a given plan.  At the default plan (8) every config-B / E
+// level keeps kc = 1.  Measured (graph-loop step, same box, r06q): planned batch 1,
+// B = 1 64^2 2.60 -> 2.52 ms, config A 2.17 -> 2.09 ms; a 16^2 split at plan 8
+// (192 -> 384 workgroups) cost B = 8 +0.7 %, hence the bound.
+int attention_kv_chunks(int T, int heads, int plan_b) {
+#ifdef CFD_ATTN_NO_KC   // development A/B build (make VARIANT=... VFLAGS=-DCFD_ATTN_NO_KC)
+    return 1;
+#endif
+    const int nblk = (T + 31) / 32;
+    const int64_t wgs = (int64_t)plan_b * heads * ceil_div(T, 64);
+    int kc = 1;
+    while (kc * 4 <= nblk && wgs * kc * 2 <= 256) kc *= 2;
+    return kc;
+}
+
+size_t attention_part_floats(int T, int C, int CH, int plan_b) {
+    const int heads = C / CH, kc = attention_kv_chunks(T, heads, plan_b);
+    return kc == 1 ? 0 : (size_t)kc * T * (C + 2 * heads);
+}
+
+void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, int plan_b, float* kvws, hipStream_t st,
+                            bool packed) {
     CFD_REQUIRE(CH == 32 || CH == 64 || CH == 128, CFD_ESHAPE, "split attention needs head channels 32, 64 or 128");
     const int T32 = (a.T + 31) / 32 * 32;
     h8v* kf = (h8v*)kvws;
@@ -2139,6 +2216,29 @@ void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* 
         hipLaunchKernelGGL(attn_kv_split_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, st, a, CH, heads,
                            B, kf, vf);
         check_launch("attn_kv_split_kernel");
+    }
+    const int kc = attention_kv_chunks(a.T, heads, plan_b);
+    if (kc > 1) {
+        CFD_REQUIRE(a.part, CFD_ESTATE, "internal: key-chunked attention without a partial buffer");
+        AttnArgs a2 = a;
+        a2.kc = kc;
+        a2.xcdmap = 0;
+        const dim3 grid((unsigned)ceil_div(a.T, 64), heads, B * kc);
+        switch (CH) {
+            case 32: hipLaunchKernelGGL((attention_dma_kernel<32, 4, 3, true>), grid, dim3(256), 0, st, a2, kf, vf); break;
+            case 64: hipLaunchKernelGGL((attention_dma_kernel<64, 4, 3, true>), grid, dim3(256), 0, st, a2, kf, vf); break;
+            default: hipLaunchKernelGGL((attention_dma_kernel<128, 4, 3, true>), grid, dim3(256), 0, st, a2, kf, vf); break;
+        }
+        check_launch("attention_dma_kernel (key chunks)");
+        const int64_t n = (int64_t)B * heads * a.T * (CH / 4);
+        const dim3 g2((unsigned)ceil_div(n, 256));
+        switch (CH) {
+            case 32: hipLaunchKernelGGL(attn_combine_kernel<32>, g2, dim3(256), 0, st, a2, heads, B); break;
+            case 64: hipLaunchKernelGGL(attn_combine_kernel<64>, g2, dim3(256), 0, st, a2, heads, B); break;
+            default: hipLaunchKernelGGL(attn_combine_kernel<128>, g2, dim3(256), 0, st, a2, heads, B); break;
+        }
+        check_launch("attn_combine_kernel");
+        return;
     }
     // K4d: fragments staged per workgroup by LDS-DMA, 8 waves (128 queries) per
     // workgroup where T >= 512 and that still gives >= 256 workgroups, else 4 -- at

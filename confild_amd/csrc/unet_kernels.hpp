@@ -95,6 +95,10 @@ struct AttnArgs {
     // K4d: workgroups of one (sample, head) on one XCD (set by the launcher where
     // heads * B % 8 == 0), so its K/V fragments are fetched into one L2
     int xcdmap;
+    // key-chunked launches (attention_kv_chunks > 1): chunk count, and the per-chunk
+    // partials (O unnormalised, then (max, sum) pairs) the combine pass reduces
+    int kc;
+    float* part;
 };
 
 // GroupNorm(32)(+SiLU) backward: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),
@@ -212,8 +216,13 @@ void launch_attention(const AttnArgs& a, int CH, int heads, int B, hipStream_t s
 // split-f16 attention (K4s); kvws holds attention_split_floats(T, C) floats per sample
 size_t attention_split_floats(int T, int C);
 // packed: the qkv convolution already wrote the K / V fragments (ConvArgs::kvf)
-void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, float* kvws, hipStream_t st,
-                            bool packed = false);
+// key chunks of the split attention at this shape and planned batch (a function of
+// neither the real batch nor the data: batch invariance), and their partials' floats
+// per sample
+int attention_kv_chunks(int T, int heads, int plan_b);
+size_t attention_part_floats(int T, int C, int CH, int plan_b);
+void launch_attention_split(const AttnArgs& a, int CH, int heads, int B, int plan_b, float* kvws, hipStream_t st,
+                            bool packed);
 // the K / V fragment pointers of kvws (launch_attention_split's layout): K at
 // kvws, V at kvws + voff h8v
 int64_t attention_split_voff(int T, int CH, int heads, int B);

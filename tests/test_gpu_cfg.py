@@ -216,11 +216,15 @@ BF16_SAMPLE_1000, BF16_EPS_1000 = 2.4e-2, 7.5e-2
 BF16_SAMPLE_100, BF16_X0_100 = 1.1e-3, 2e-2
 
 
-def test_configA_ddim50_and_decode_end_to_end(hip):
+@pytest.mark.parametrize("plan", [0, 1], ids=["plan8", "plan1"])
+def test_configA_ddim50_and_decode_end_to_end(hip, plan):
+    """Config A end to end at the default planned batch and at 1 (the plan the
+    config-A line is timed at: one sample per GPU; key-chunked attention at 32^2)."""
     from confild_amd.inference import latent_denorm
     c = CFG_A
     g = golden("golden_cfgA.npz")
     m = _unet(c)
+    m.set_plan_batch(plan)
     d = create_gaussian_diffusion(steps=1000, noise_schedule="cosine", timestep_respacing=c["respacing"])
     assert np.array_equal(np.asarray(d.timestep_map), g["timestep_map"])
     S = c["image_size"]

@@ -24,7 +24,8 @@ def model(size, mult, compute="split_f16"):
                      attention_resolutions="32,16,8", channel_mult=mult)
     sd = synth.unet_state_dict(1234, {k: tuple(v.shape) for k, v in m.state_dict().items()})
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    return m.to(DEV).set_compute(compute)
+    m = m.to(DEV).set_compute(compute)
+    return m.set_plan_batch(int(os.environ.get("LOOP_PLAN", "0")))   # LOOP_PLAN: the planned batch
 
 
 def forward_ms(m, B, size, iters=20):
