@@ -300,7 +300,13 @@ class PipelineB:
     def __init__(self, o, dev, start, count, sizes, world, gather, sample_cus=None, split=True):
         from confild_amd.streams import CuRangeStream, cu_count
         n = cu_count(dev)
-        h = n // 2 if sample_cus is None else int(sample_cus)   # CUs of the sampling half
+        # CUs of the sampling stream: half the chip, three quarters where the decode is
+        # small (<= 2 samples per batch: the 8-GPU strong share; 128 / 160 / 192 / 224
+        # CUs measured 709 / 697 / 692 / 745 ms per one-sample batch, profiles/r06u_*)
+        if sample_cus is None:
+            h = n * 3 // 4 if count * S <= 128 else n // 2
+        else:
+            h = int(sample_cus)
         self.su = CuRangeStream(dev, 0, h)
         self.sd = CuRangeStream(dev, h, n - h)
         self.cus = (h, n - h)

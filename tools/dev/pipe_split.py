@@ -3,6 +3,7 @@ the sampling and the decode streams (development tool): fields/s over K timed
 batches after W warmup batches, per split, in one process.
 
     python tools/dev/pipe_split.py 96 112 128 144 160
+    PIPE_COUNT=1 PIPE_PLAN=1 python tools/dev/pipe_split.py 128 160 192 224   # the strong share
 """
 import json
 import os
@@ -21,19 +22,20 @@ DEV = torch.device("cuda", 0)
 def main():
     splits = [int(v) for v in sys.argv[1:]] or [128]
     W, K = 3, 8
-    o = bench.setup_B(DEV, 0, 1, "split_f16", "split_f16")
-    R = 8 * bench.S
+    count = int(os.environ.get("PIPE_COUNT", "8"))
+    o = bench.setup_B(DEV, 0, 1, "split_f16", "split_f16", plan_batch=int(os.environ.get("PIPE_PLAN", "0")))
+    R = count * bench.S
     out = []
     for rnd in range(2):
         for h in splits:
-            with bench.PipelineB(o, DEV, 0, 8, [R], 1, False, sample_cus=h) as pp:
+            with bench.PipelineB(o, DEV, 0, count, [R], 1, False, sample_cus=h) as pp:
                 pp.run([10 ** 6 + k for k in range(W)])
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 pp.run([2 * 10 ** 6 + k for k in range(K)])
                 torch.cuda.synchronize()
                 el = time.perf_counter() - t0
-            rec = {"round": rnd, "sample_cus": h, "fields_per_s": 8 * K / el, "ms_per_batch": el / K * 1e3,
+            rec = {"round": rnd, "count": count, "sample_cus": h, "fields_per_s": count * K / el, "ms_per_batch": el / K * 1e3,
                    "rows_b": pp.rows_b[-3:]}
             out.append(rec)
             print(json.dumps(rec), flush=True)
