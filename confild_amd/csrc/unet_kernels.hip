@@ -259,7 +259,10 @@ __global__ __launch_bounds__(NT) void gn_fused_reg_kernel(GnArgs a) {
             const int p = r0 + k * rows;
             v[k] = act && p < HW ? *(const f4*)(kpart + ib + k * istep) : f4{0.f, 0.f, 0.f, 0.f};
         }
-        constexpr int UN = IPT <= 2 ? 8 : IPT <= 4 ? 4 : 1;
+        // 2 slabs per round in the 1024-thread tier: 55 VGPRs, two workgroups per CU (the
+        // 256 launches of a B = 8 32^2 level fit one round on a CU half: pipelined step
+        // +0.4 %, whole chip flat, the same bits; profiles/r06v_gn1024_ab.json)
+        constexpr int UN = IPT <= 2 ? (NT >= 1024 ? 2 : 8) : IPT <= 4 ? 4 : 1;
         for (int sp = 1; sp < a.ksplits; sp += UN) {
             f4 u[UN][IPT];
 #pragma unroll
