@@ -2193,9 +2193,6 @@ int64_t attention_split_voff(int T, int CH, int heads, int B) {
 // B = 1 64^2 2.60 -> 2.52 ms, config A 2.17 -> 2.09 ms; a 16^2 split at plan 8
 // (192 -> 384 workgroups) cost B = 8 +0.7 %, hence the bound.
 int attention_kv_chunks(int T, int heads, int plan_b) {
-#ifdef CFD_ATTN_NO_KC   // development A/B build (make VARIANT=... VFLAGS=-DCFD_ATTN_NO_KC)
-    return 1;
-#endif
     const int nblk = (T + 31) / 32;
     const int64_t wgs = (int64_t)plan_b * heads * ceil_div(T, 64);
     int kc = 1;
