@@ -11,5 +11,5 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 extern "C" const char* cfd_last_error(void) { return cfd::g_last_error.c_str(); }
 
 extern "C" const char* cfd_version(void) {
-    return "libconfild_hip gfx950 r5 (split-f16 / bf16 / fp32 MFMA; native sampler graphs; planned batch; CU-range streams)";
+    return "libconfild_hip gfx950 r6 (split-f16 / bf16 / fp32 MFMA; native sampler graphs; planned batch; CU-range streams; split-f16 DPS tape; key-chunked attention)";
 }
